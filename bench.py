@@ -1,0 +1,249 @@
+"""Benchmark of the geodesic ray-tracing hot path (BASELINE.json metric) on MI355X.
+
+One "step" = one camera frame of the workload traced by libbhrt.so with every input already
+on the device: the frame kernel launch, plus (N > 1) the single RCCL gather of all shards to
+rank 0 and the device-side un-permute of the cyclic row blocks into the final image.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--camera B]
+
+N > 1 is launched by torch.distributed.run, one process per GPU. Weak scaling: every GPU owns
+a full configuration-sized shard (1920 x 1080 pixels for C2) of an image 1080*N rows tall,
+assigned as cyclic 8-row blocks so the divergent disk band spreads evenly.
+
+The JSON line also carries:
+  roofline      FP64 VALU roofline of the trace kernel: algorithmic FLOPs (SURVEY.md 8(a):
+                117 per RK4 iteration + 35 per a=0 derivative stage + 4 per far-field stage;
+                368 per RKF45 attempt + the same stage costs) / the kernel's HIP-event time.
+  cpu_baseline  the compiled reference (oracle/_ref/libref.so, unmodified trace_ray under an
+                OpenMP loop) on a row sample of the same frame, rank 0 at N = 1 only; its
+                sampled rows double as the parity check "max |dhit|".
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from bhrt import abi, configs, lib  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (and FP64 matrix) peak, AMD spec
+METRIC = "Mrays/s (and RK4 steps/s) per GPU + per node; max |Δhit| vs CPU ref"
+ROW_BLOCK = 8
+FIELDS = abi.SOA_FIELDS
+INT_FIELDS = ("result", "steps")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--config", default="C2")
+    p.add_argument("--camera", default="B")
+    p.add_argument("--refill", type=int, default=None)
+    p.add_argument("--cpu-rows-stride", type=int, default=27,
+                   help="CPU baseline samples every k-th image row")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def flops(st, method):
+    per_iter = 368 if method == abi.INTEGRATOR_RKF45 else 117
+    return per_iter * st["iterations"] + 35 * st["stages_full"] + 4 * st["stages_far"]
+
+
+class Frame:
+    """Device SoA of one shard, carved from ONE byte buffer so the gather is one collective."""
+
+    def __init__(self, n, device):
+        self.n = n
+        sizes = [4 if f in INT_FIELDS else 8 for f in FIELDS]
+        self.offsets = np.concatenate([[0], np.cumsum([s * n for s in sizes])]).astype(int)
+        self.buf = torch.empty(int(self.offsets[-1]), dtype=torch.uint8, device=device)
+        self.views = {}
+        for i, f in enumerate(FIELDS):
+            dt = torch.int32 if f in INT_FIELDS else torch.float64
+            self.views[f] = self.buf[self.offsets[i]:self.offsets[i + 1]].view(dt)
+        self.soa = lib.soa_from_tensors(self.views)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    L = lib.load()
+    if args.refill:
+        L.bhrt_set_refill_threshold(args.refill)
+
+    c = configs.CONFIGS[args.config]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera(args.camera)
+    W, H1 = c.width, c.height
+    H = H1 * world
+    rows = abi.Rows(ROW_BLOCK, rank, world)
+    n_rows = lib.shard_rows(H, rows)
+    n = n_rows * W
+    frame = Frame(n, device)
+    stream = torch.cuda.current_stream()
+    gathered = [torch.empty_like(frame.buf) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    def step():
+        lib.render_frame_device(bh, dk, cfg, cam, W, H, rows if world > 1 else None, c.method,
+                                c.flags, frame.soa, stream.cuda_stream)
+        if world > 1:
+            dist.gather(frame.buf, gathered, dst=0)
+            if rank == 0:  # un-permute cyclic row blocks into the H x W image
+                img = {}
+                for i, f in enumerate(FIELDS):
+                    dt = torch.int32 if f in INT_FIELDS else torch.float64
+                    parts = torch.stack([g[frame.offsets[i]:frame.offsets[i + 1]].view(dt)
+                                         for g in gathered])
+                    img[f] = (parts.view(world, n_rows // ROW_BLOCK, ROW_BLOCK, W)
+                              .permute(1, 0, 2, 3).reshape(H, W))
+                return img
+        return None
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    lib.stats(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = lib.stats(reset=True)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        tot = torch.tensor([st["iterations"]], dtype=torch.float64, device=device)
+        dist.all_reduce(tot)
+        iterations_all = tot.item()
+    else:
+        iterations_all = st["iterations"]
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    rays_all = float(W * H) * args.steps
+    mrays = rays_all / elapsed / 1e6
+    kern_ms = st["kernel_ms"] / max(st["launches"], 1)
+    f_launch = flops(st, c.method) / max(st["launches"], 1)
+    achieved = f_launch / (kern_ms * 1e-3) / 1e12
+    out = {
+        "metric": METRIC,
+        "value": round(mrays, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (deterministic camera-B frame, no input data)",
+        "config": {
+            "workload": f"{c.name}: {c.note}",
+            "camera": args.camera,
+            "width": W,
+            "height": H,
+            "rays_per_gpu": n,
+            "parallelism": (f"dp{world}: cyclic {ROW_BLOCK}-row blocks, one RCCL gather to rank 0"
+                            if world > 1 else "single GPU"),
+        },
+        "rk4_steps_per_s": round(iterations_all * (1.0 / elapsed), 1),
+        "per_gpu_mrays_s": round(mrays / world, 3),
+        "kernel": {
+            "name": "k_trace (persistent, wave refill)",
+            "avg_ms": round(kern_ms, 4),
+            "iterations_per_launch": st["iterations"] / max(st["launches"], 1),
+            "mean_iterations_per_ray": st["iterations"] / max(st["rays"], 1),
+        },
+        "roofline": {
+            "bound": "valu-fp64",
+            "achieved": round(achieved, 4),
+            "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
+            "traffic": traffic_from_profile(args.config),
+        },
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"], out["max_rel_dhit"], out["class_mismatch"] = cpu_baseline(
+            args, c, bh, dk, cfg, cam, frame)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def traffic_from_profile(config):
+    """HBM bytes per trace-kernel launch from the committed rocprofv3 PMC summary (FETCH_SIZE
+    x2 per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md 'HBM'), or None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(args, c, bh, dk, cfg, cam, frame):
+    """The compiled reference (or, if it was not built, the oracle restatement) on every k-th
+    row of the same frame; also the parity of those rows against the GPU frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    try:
+        checker, kind = orc.reference(), "reference"
+    except (FileNotFoundError, OSError):
+        checker, kind = orc.oracle(), "port"
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    W, H = c.width, c.height
+    rows = list(range(0, H, args.cpu_rows_stride))
+    got = {f: frame.views[f].view(-1).cpu().numpy().reshape(H, W)[rows] for f in FIELDS}
+    t0 = time.perf_counter()
+    want = []
+    for r in rows:
+        want.append(checker.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags,
+                                         rows=abi.Rows(1, r, H), threads=threads))
+    dt = time.perf_counter() - t0
+    nrays = len(rows) * W
+    want = {f: np.stack([w[f] for w in want]) for f in FIELDS}
+    mism = int((got["result"] != want["result"]).sum() + (got["steps"] != want["steps"]).sum())
+    worst = 0.0
+    for f in ("hit_x", "hit_y", "hit_z", "distance", "time_dilation", "rgb_r", "rgb_g", "rgb_b"):
+        a, b = got[f], want[f]
+        ok = ~(np.isnan(a) | np.isnan(b))
+        if ok.any():
+            worst = max(worst, float(np.max(np.abs(a[ok] - b[ok]) /
+                                            np.maximum(np.abs(b[ok]), 1e-9))))
+    base = {"value": round(nrays / dt / 1e6, 5), "unit": "Mrays/s", "cores": threads,
+            "kind": kind,
+            "sample": f"rows 0,{args.cpu_rows_stride},... of the {W}x{H} frame ({nrays} rays, "
+                      f"{dt:.1f} s wall, OpenMP over rays; the reference integrates every ray "
+                      f"to its full step budget before the disk scan)"}
+    return base, worst, mism
+
+
+if __name__ == "__main__":
+    main()

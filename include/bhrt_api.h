@@ -1,0 +1,245 @@
+/*
+ * bhrt_api.h -- C ABI of libbhrt.so, the MI355X geodesic ray tracer.
+ *
+ * Two groups of entry points:
+ *
+ *  1. Drop-in: the reference engine's own symbols, same names, arguments, return codes and
+ *     struct layouts (bhrt_types.h). Each declaration names the reference interface it
+ *     replaces. The ray-tracing ones (trace_ray, trace_rays_batch, integrate_photon_path,
+ *     trace_pixel, bh_trace_ray, bh_trace_rays_batch) run on the GPU; there is no CPU
+ *     fallback: if HIP is unavailable they return the reference's error value and
+ *     bhrt_last_error() says why.
+ *
+ *  2. Extension (bhrt_*): whole-frame rendering with device-resident SoA outputs, row
+ *     sharding for multi-GPU, and launch statistics. This is what bench.py drives.
+ *
+ * Host buffers are always caller-owned; nothing is retained across calls.
+ */
+#ifndef BHRT_API_H
+#define BHRT_API_H
+
+#include "bhrt_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLACKHOLE_API_VERSION_MAJOR 0
+#define BLACKHOLE_API_VERSION_MINOR 1
+#define BLACKHOLE_API_VERSION_PATCH 0
+
+#define BH_PI 3.14159265358979323846
+#define BH_EPSILON 1.0e-10
+#define BH_TWO_PI 6.28318530717958647692
+
+typedef enum {
+    BH_SUCCESS = 0,
+    BH_ERROR_INVALID_PARAMETER = -1,
+    BH_ERROR_MEMORY_ALLOCATION = -2,
+    BH_ERROR_INITIALIZATION = -3,
+    BH_ERROR_SIMULATION = -4
+} BHErrorCode; /* include/blackhole_api.h:30-36 */
+
+typedef struct BHContext_t* BHContextHandle; /* include/blackhole_api.h:40 */
+
+/* ================================ 1. drop-in symbols ==================================== */
+
+/* --- ray tracing (GPU) --- */
+
+/* replaces raytracer.h:129-133 / src/raytracer.c:684-767 */
+RayTraceResult trace_ray(const Ray* ray, const BlackHoleParams* blackhole,
+                         const AccretionDiskParams* disk, const SimulationConfig* config,
+                         RayTraceHit* hit);
+
+/* replaces raytracer.h:205-212 / src/raytracer.c:782-807. Returns -1 if rays, blackhole or
+ * hits is NULL or num_rays <= 0, else 0. num_threads is ignored (the GPU decides). */
+int trace_rays_batch(const Ray* rays, int num_rays, const BlackHoleParams* blackhole,
+                     const AccretionDiskParams* disk, const SimulationConfig* config,
+                     RayTraceHit* hits, int num_threads);
+
+/* replaces raytracer.h:181-190 / src/raytracer.c:338-679 */
+RayTraceResult integrate_photon_path(const Vector4D* position, const Vector3D* direction,
+                                     const BlackHoleParams* blackhole,
+                                     const SimulationConfig* config, IntegrationMethod method,
+                                     Vector3D* path_positions, int max_positions,
+                                     int* num_positions, RayTraceHit* hit);
+
+/* replaces raytracer.h:151-165 / src/raytracer.c:1044-1167 (see DESIGN.md for the colour
+ * of disk samples, which the reference reads from an uninitialised field) */
+RayTraceResult trace_pixel(int pixel_x, int pixel_y, int width, int height,
+                           const Vector3D* camera_position, const Vector3D* camera_direction,
+                           const Vector3D* camera_up, double fov,
+                           const BlackHoleParams* blackhole, const AccretionDiskParams* disk,
+                           const SimulationConfig* config, const SupersamplingParams* ss_params,
+                           const AdaptiveSamplingParams* as_params, double color_out[3]);
+
+/* --- ray-path helpers (host scalar code, same arithmetic as the device) --- */
+int check_disk_intersection(const Vector3D* position, const Vector3D* velocity,
+                            const Vector3D* prev_position, const AccretionDiskParams* disk,
+                            Vector3D* hit_position);                     /* raytracer.c:159 */
+void calculate_disk_temperature(const Vector3D* position, const BlackHoleParams* blackhole,
+                                const AccretionDiskParams* disk, double* temperature,
+                                double color[3]);                        /* raytracer.c:201 */
+void apply_relativistic_effects(const Vector3D* position, const Vector3D* velocity,
+                                const BlackHoleParams* blackhole, double color[3],
+                                double* doppler_factor);                 /* raytracer.c:233 */
+void generate_gpu_shader_params(const BlackHoleParams* blackhole,
+                                const AccretionDiskParams* disk, double observer_distance,
+                                double fov, GPUShaderParams* params);     /* raytracer.c:818 */
+double halton_sequence(int index, int base);                             /* raytracer.c:852 */
+
+/* spacetime.h */
+void initialize_black_hole_params(BlackHoleParams* blackhole, double mass, double spin,
+                                  double charge);                        /* spacetime.c:331 */
+double get_isco_radius(const BlackHoleParams* blackhole);                /* spacetime.c:285 */
+SchwarzschildMetric calculate_schwarzschild_metric(double r, const BlackHoleParams* bh);
+                                                                         /* spacetime.c:15 */
+double calculate_time_dilation(double r, const BlackHoleParams* blackhole);/* spacetime.c:192 */
+void cartesian_to_spherical(const Vector3D* cartesian, Vector3D* spherical);/* spacetime.c:201 */
+void spherical_to_cartesian(const Vector3D* spherical, Vector3D* cartesian);/* spacetime.c:229 */
+
+/* math_util.h */
+Vector3D vector3D_add(const Vector3D a, const Vector3D b);               /* math_util.c:31 */
+Vector3D vector3D_sub(const Vector3D a, const Vector3D b);               /* math_util.c:49 */
+Vector3D vector3D_scale(const Vector3D v, double scale);                 /* math_util.c:67 */
+double   vector3D_dot(const Vector3D a, const Vector3D b);               /* math_util.c:85 */
+Vector3D vector3D_cross(const Vector3D a, const Vector3D b);             /* math_util.c:100 */
+double   vector3D_length(const Vector3D v);                              /* math_util.c:111 */
+Vector3D vector3D_normalize(const Vector3D v);                           /* math_util.c:115 */
+void rk4_integrate(ODEFunction f, double* y, int n, double t, double h, void* params);
+                                                                         /* math_util.c:162 */
+int rkf45_integrate(ODEFunction f, double y[], int n, double* t, double h_try, double* h_next,
+                    double eps_rel, void* params);                       /* math_util.c:212 */
+void temperature_to_rgb(double temperature, double rgb[3]);              /* math_util.c:463 */
+double clamp(double value, double min, double max);                      /* math_util.c:505 */
+
+/* --- context API (include/blackhole_api.h:47-255, src/blackhole_api.c) --- */
+BHContextHandle bh_initialize(void);                                     /* blackhole_api.c:52 */
+void bh_shutdown(BHContextHandle context);                               /* blackhole_api.c:85 */
+double blackhole_get_mass(BHContextHandle context);                      /* blackhole_api.c:33 */
+void bh_calculate_orbital_velocity(BHContextHandle context, double r, double* v_phi);
+                                                                         /* blackhole_api.c:42 */
+BHErrorCode bh_configure_black_hole(BHContextHandle context, double mass, double spin,
+                                    double charge);                      /* blackhole_api.c:94 */
+BHErrorCode bh_configure_accretion_disk(BHContextHandle context, double inner_radius,
+                                        double outer_radius, double temperature_scale,
+                                        double density_scale);           /* blackhole_api.c:123 */
+BHErrorCode bh_configure_simulation(BHContextHandle context, double time_step,
+                                    double max_ray_distance, int max_integration_steps,
+                                    double tolerance);                   /* blackhole_api.c:153 */
+BHErrorCode bh_trace_ray(BHContextHandle context, const double origin[3],
+                         const double direction[3], RayTraceHit* hit);   /* blackhole_api.c:182 */
+BHErrorCode bh_trace_rays_batch(BHContextHandle context, const Ray* rays, RayTraceHit* hits,
+                                int count);                              /* blackhole_api.c:225 */
+BHErrorCode bh_calculate_time_dilation(BHContextHandle context, const double position1[3],
+                                       const double position2[3], double* time_ratio);
+                                                                         /* blackhole_api.c:432 */
+void bh_get_version(int* major, int* minor, int* patch);                 /* blackhole_api.c:464 */
+BHErrorCode bh_generate_shader_data(void* context, const float observer_pos[3],
+                                    const float observer_dir[3], const float up_vector[3],
+                                    int width, int height, float fov, int enable_doppler,
+                                    int enable_redshift, int show_disk, float* output_buffer);
+                                                                         /* blackhole_api.c:495 */
+
+/* ================================ 2. bhrt extension ===================================== */
+
+/* Pinhole camera of trace_pixel/calculate_ray_direction (raytracer.c:999-1039); fov in
+ * degrees; pixel-centre rays (offset 0.5, 0.5). */
+typedef struct {
+    Vector3D position;
+    Vector3D direction;
+    Vector3D up;
+    double   fov_deg;
+} bhrt_camera;
+
+/* Frame flags */
+#define BHRT_FLAG_DOPPLER 1 /* disk colour through apply_relativistic_effects (config C4) */
+
+/* Structure-of-arrays frame. Element i is the i-th ray of the launch (for a camera frame:
+ * the i-th pixel of the shard, row-major over the shard's rows). Any pointer may be NULL,
+ * in which case that field is not produced. Pointers are device pointers for the *_device
+ * calls and host pointers otherwise. */
+typedef struct {
+    int32_t* result;        /* RayTraceResult                                            */
+    int32_t* steps;         /* RayTraceHit.steps                                         */
+    double*  hit_x;         /* RayTraceHit.hit_position                                  */
+    double*  hit_y;
+    double*  hit_z;
+    double*  distance;
+    double*  time_dilation;
+    double*  sky_x;         /* RayTraceHit.sky_direction, written for MAX_DISTANCE only  */
+    double*  sky_y;
+    double*  sky_z;
+    double*  rgb_r;         /* frame colour contract, DESIGN.md section 3                */
+    double*  rgb_g;
+    double*  rgb_b;
+} bhrt_frame_soa;
+
+/* Cyclic row-block sharding of an image across num_shards GPUs: block b (rows
+ * [b*row_block, (b+1)*row_block)) belongs to shard b % num_shards. {0,0,1} = whole image. */
+typedef struct {
+    int row_block;
+    int shard;
+    int num_shards;
+} bhrt_rows;
+
+/* Launch statistics accumulated on the calling thread since the last reset. */
+typedef struct {
+    uint64_t rays;          /* rays traced                                               */
+    uint64_t iterations;    /* executed RK4 iterations / RKF45 attempts                  */
+    uint64_t stages_full;   /* ray_derivatives evaluations, a=0 strong-field branch      */
+    uint64_t stages_far;    /* ... far-field branch                                      */
+    uint64_t stages_kerr;   /* ... spin != 0 branch                                      */
+    uint64_t launches;      /* trace-kernel launches timed                               */
+    double   kernel_ms;     /* sum of HIP-event durations of those launches              */
+} bhrt_stats;
+
+/* Number of rows of an image of `height` rows owned by shard rows->shard. */
+int bhrt_shard_rows(int height, const bhrt_rows* rows);
+
+/* Render (a shard of) a camera frame into DEVICE SoA buffers on `hip_stream` (a
+ * hipStream_t; NULL = the library's per-thread stream). Asynchronous: returns after the
+ * launch. Returns 0, or -1 on invalid arguments / HIP failure (see bhrt_last_error). */
+int bhrt_render_frame_device(const BlackHoleParams* blackhole, const AccretionDiskParams* disk,
+                             const SimulationConfig* config, const bhrt_camera* camera,
+                             int width, int height, const bhrt_rows* rows,
+                             IntegrationMethod method, int flags,
+                             const bhrt_frame_soa* device_out, void* hip_stream);
+
+/* Same, into HOST buffers; splits the image over every visible GPU (cyclic row blocks)
+ * and returns when the frame is complete. */
+int bhrt_render_frame(const BlackHoleParams* blackhole, const AccretionDiskParams* disk,
+                      const SimulationConfig* config, const bhrt_camera* camera, int width,
+                      int height, IntegrationMethod method, int flags,
+                      const bhrt_frame_soa* host_out);
+
+/* Trace n rays already resident on the device (AoS Ray[n]) into DEVICE SoA buffers.
+ * method RK4 with disk != NULL is trace_ray; RKF45 with a disk is integrate_photon_path
+ * plus trace_ray's disk scan (config C3). */
+int bhrt_trace_rays_device(const Ray* device_rays, int n, const BlackHoleParams* blackhole,
+                           const AccretionDiskParams* disk, const SimulationConfig* config,
+                           IntegrationMethod method, int flags,
+                           const bhrt_frame_soa* device_out, void* hip_stream);
+
+/* Host-buffer variant of the above (host Ray[n] in, host SoA out), multi-GPU split. */
+int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* blackhole,
+                    const AccretionDiskParams* disk, const SimulationConfig* config,
+                    IntegrationMethod method, int flags, const bhrt_frame_soa* host_out);
+
+/* Copy and optionally reset this thread's statistics (waits for the timed launches). */
+int bhrt_get_stats(bhrt_stats* out, int reset);
+
+/* Number of GPUs libbhrt will use (HIP_VISIBLE_DEVICES / BHRT_MAX_DEVICES respected). */
+int bhrt_device_count(void);
+
+/* Tuning knob: refill a wavefront's finished lanes once at least this many are idle
+ * (1..64, default 8). Affects speed only. */
+void bhrt_set_refill_threshold(int lanes);
+
+/* Last error message of the calling thread ("" if none). */
+const char* bhrt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BHRT_API_H */

@@ -1,0 +1,1176 @@
+/*
+ * bhrt_api.c -- host side of libbhrt.so, in C (C11), calling HIP through the C runtime API
+ * and the two launchers of geodesic.hip.
+ *
+ * Drop-in entry points keep the reference's argument checks and return codes
+ * (src/raytracer.c, src/blackhole_api.c); the ray tracing itself always runs on the GPU.
+ * There is no CPU fallback: a HIP failure is reported through the reference's error value
+ * (RAY_ERROR / -1 / BH_ERROR_SIMULATION) and bhrt_last_error().
+ *
+ * Device state is per (host thread, device): a stream, growable device buffers and a ring
+ * of control blocks (queue head + counters) with start/stop events per launch, so
+ * trace_ray / trace_rays_batch stay callable concurrently from several host threads
+ * (SURVEY.md 8b "Threading").
+ */
+#define _GNU_SOURCE
+#include <hip/hip_runtime_api.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#pragma GCC visibility push(default)
+#include "../../include/bhrt_api.h"
+#pragma GCC visibility pop
+#include "bhrt_kernel.h"
+
+/* ======================================================================================= */
+/* errors                                                                                  */
+/* ======================================================================================= */
+static _Thread_local char g_err[256];
+
+static void set_err(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    if (getenv("BHRT_VERBOSE")) fprintf(stderr, "libbhrt: %s\n", g_err);
+}
+
+const char* bhrt_last_error(void) { return g_err; }
+
+#define HIP_TRY(call)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            set_err("%s failed: %s", #call, hipGetErrorString(e_));                           \
+            return -1;                                                                        \
+        }                                                                                     \
+    } while (0)
+
+/* ======================================================================================= */
+/* host vector helpers (math_util.c:31-122 semantics; also the drop-in vector3D_* symbols)  */
+/* ======================================================================================= */
+Vector3D vector3D_add(const Vector3D a, const Vector3D b) {
+    Vector3D r = {a.x + b.x, a.y + b.y, a.z + b.z};
+    return r;
+}
+Vector3D vector3D_sub(const Vector3D a, const Vector3D b) {
+    Vector3D r = {a.x - b.x, a.y - b.y, a.z - b.z};
+    return r;
+}
+Vector3D vector3D_scale(const Vector3D v, double s) {
+    Vector3D r = {v.x * s, v.y * s, v.z * s};
+    return r;
+}
+double vector3D_dot(const Vector3D a, const Vector3D b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+Vector3D vector3D_cross(const Vector3D a, const Vector3D b) {
+    Vector3D r = {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+    return r;
+}
+double vector3D_length(const Vector3D v) { return sqrt(vector3D_dot(v, v)); }
+Vector3D vector3D_normalize(const Vector3D v) {
+    double l = vector3D_length(v);
+    if (l < BH_EPSILON) {
+        Vector3D z = {0.0, 0.0, 0.0};
+        return z;
+    }
+    return vector3D_scale(v, 1.0 / l);
+}
+double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* ======================================================================================= */
+/* device contexts                                                                          */
+/* ======================================================================================= */
+#define BHRT_MAX_DEV 16
+#define BHRT_RING 64        /* control blocks per context             */
+#define BHRT_CTL_WORDS 8    /* u64 per control block (64 B)           */
+#define BHRT_NFIELDS 13
+
+typedef struct {
+    int slot;
+    hipEvent_t ev0, ev1;
+} pending_t;
+
+typedef struct {
+    int device;
+    hipStream_t stream;
+    unsigned long long* d_ctl; /* BHRT_RING x BHRT_CTL_WORDS */
+    pending_t pend[BHRT_RING];
+    int npend, next_slot;
+    hipEvent_t evpool[2 * BHRT_RING];
+    /* growable device buffers */
+    void* d_rays;
+    size_t cap_rays;
+    void* d_soa;
+    size_t cap_soa; /* rays */
+    void* h_stage;  /* pinned staging for SoA readback */
+    size_t cap_stage;
+    void* d_init;   /* initial-state table of ray-array launches */
+    size_t cap_init;
+} devctx_t;
+
+static _Thread_local devctx_t* g_ctx[BHRT_MAX_DEV];
+static _Thread_local bhrt_stats g_stats;
+static int g_refill = 8;
+
+void bhrt_set_refill_threshold(int lanes) {
+    g_refill = lanes < 1 ? 1 : (lanes > 64 ? 64 : lanes);
+}
+
+int bhrt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    const char* cap = getenv("BHRT_MAX_DEVICES");
+    if (cap && atoi(cap) > 0 && atoi(cap) < n) n = atoi(cap);
+    if (n > BHRT_MAX_DEV) n = BHRT_MAX_DEV;
+    return n;
+}
+
+static devctx_t* ctx_get(int device) {
+    if (device < 0 || device >= BHRT_MAX_DEV) {
+        set_err("device %d out of range", device);
+        return NULL;
+    }
+    if (g_ctx[device]) return g_ctx[device];
+    if (hipSetDevice(device) != hipSuccess) {
+        set_err("hipSetDevice(%d) failed", device);
+        return NULL;
+    }
+    devctx_t* c = (devctx_t*)calloc(1, sizeof *c);
+    if (!c) return NULL;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void**)&c->d_ctl, BHRT_RING * BHRT_CTL_WORDS * sizeof(unsigned long long)) !=
+            hipSuccess) {
+        set_err("cannot create HIP stream / control blocks on device %d", device);
+        free(c);
+        return NULL;
+    }
+    for (int i = 0; i < 2 * BHRT_RING; i++)
+        if (hipEventCreate(&c->evpool[i]) != hipSuccess) {
+            set_err("hipEventCreate failed");
+            free(c);
+            return NULL;
+        }
+    g_ctx[device] = c;
+    return c;
+}
+
+static int ensure(void** p, size_t* cap, size_t need, int pinned) {
+    if (*cap >= need && *p) return 0;
+    size_t n = need + need / 4 + 4096;
+    if (*p) {
+        if (pinned) (void)hipHostFree(*p);
+        else (void)hipFree(*p);
+        *p = NULL;
+        *cap = 0;
+    }
+    hipError_t e = pinned ? hipHostMalloc(p, n, 0) : hipMalloc(p, n);
+    if (e != hipSuccess) {
+        set_err("allocation of %zu bytes failed: %s", n, hipGetErrorString(e));
+        *p = NULL;
+        return -1;
+    }
+    *cap = n;
+    return 0;
+}
+
+/* fold finished launches into g_stats (waits for them) */
+static int harvest(devctx_t* c) {
+    if (c->npend == 0) return 0;
+    unsigned long long h[BHRT_RING * BHRT_CTL_WORDS];
+    HIP_TRY(hipSetDevice(c->device));
+    for (int i = 0; i < c->npend; i++) HIP_TRY(hipEventSynchronize(c->pend[i].ev1));
+    HIP_TRY(hipMemcpy(h, c->d_ctl, sizeof h, hipMemcpyDeviceToHost));
+    for (int i = 0; i < c->npend; i++) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->pend[i].ev0, c->pend[i].ev1));
+        const unsigned long long* w = h + c->pend[i].slot * BHRT_CTL_WORDS;
+        g_stats.rays += w[1];
+        g_stats.iterations += w[2];
+        g_stats.stages_full += w[3];
+        g_stats.stages_far += w[4];
+        g_stats.stages_kerr += w[5];
+        g_stats.launches += 1;
+        g_stats.kernel_ms += ms;
+    }
+    c->npend = 0;
+    return 0;
+}
+
+int bhrt_get_stats(bhrt_stats* out, int reset) {
+    int rc = 0;
+    for (int d = 0; d < BHRT_MAX_DEV; d++)
+        if (g_ctx[d] && harvest(g_ctx[d]) != 0) rc = -1;
+    if (out) *out = g_stats;
+    if (reset) memset(&g_stats, 0, sizeof g_stats);
+    return rc;
+}
+
+/* ======================================================================================= */
+/* launch plumbing                                                                          */
+/* ======================================================================================= */
+static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                      const SimulationConfig* cfg, IntegrationMethod method, int flags) {
+    memset(kp, 0, sizeof *kp);
+    bhrt_scene_k* s = &kp->sc;
+    const double rs = bh->schwarzschild_radius, dt = cfg->time_step;
+    /* the products the reference forms inline (raytracer.c:65-130, 465, 556-571, 652) */
+    s->M = bh->mass;
+    s->rs = rs;
+    s->two_m = 2.0 * bh->mass;
+    s->rs_x1_5 = rs * 1.5;
+    s->rs_x1_05 = rs * 1.05;
+    s->rs_x2_5 = rs * 2.5;
+    s->rs_x5 = rs * 5.0;
+    s->rs_x15 = rs * 15.0;
+    s->rs_eps = rs + BH_EPSILON;
+    s->h_2_5 = dt * 0.001;
+    s->h_5 = dt * 0.01;
+    s->h_15 = dt * 0.1;
+    s->h_far = dt;
+    s->max_dist = cfg->max_ray_distance;
+    s->tol = cfg->tolerance;
+    s->max_steps = cfg->max_integration_steps;
+    s->method = (int)method;
+    s->flags = flags;
+    s->spin0 = bh->spin == 0.0;
+    s->has_disk = dk != NULL;
+    if (dk) {
+        s->disk_in = dk->inner_radius;
+        s->disk_out = dk->outer_radius;
+        s->disk_tscale = dk->temperature_scale;
+    }
+    kp->refill = g_refill;
+    kp->cam.rows.row_block = 1;
+    kp->cam.rows.num_shards = 1;
+    return 0;
+}
+
+/* camera basis exactly as calculate_ray_direction forms it (raytracer.c:1013-1028), and
+ * integrate_photon_path's origin-only set-up (raytracer.c:355-466, spacetime.c:15-33,
+ * 201-237): every camera ray shares the origin, so its spherical coordinates, their sin/cos
+ * and the metric there are computed once, here, with the same libm calls as the reference. */
+static void fill_camera(bhrt_kparams* kp, const bhrt_camera* cam, int W, int H) {
+    bhrt_camera_k* k = &kp->cam;
+    double aspect = (double)W / (double)H;
+    Vector3D fwd = vector3D_normalize(cam->direction);
+    Vector3D right = vector3D_normalize(vector3D_cross(fwd, cam->up));
+    Vector3D up = vector3D_cross(right, fwd);
+    double fov_radians = cam->fov_deg * BH_PI / 180.0;
+    double plane_h = 2.0 * tan(fov_radians / 2.0);
+    kp->src = BHRT_SRC_CAMERA;
+    k->fwd[0] = fwd.x; k->fwd[1] = fwd.y; k->fwd[2] = fwd.z;
+    k->right[0] = right.x; k->right[1] = right.y; k->right[2] = right.z;
+    k->up[0] = up.x; k->up[1] = up.y; k->up[2] = up.z;
+    k->plane_h = plane_h;
+    k->plane_w = plane_h * aspect;
+    k->width = W;
+    k->height = H;
+    k->pos[0] = cam->position.x;
+    k->pos[1] = cam->position.y;
+    k->pos[2] = cam->position.z;
+    Vector3D sph;
+    cartesian_to_spherical(&cam->position, &sph);
+    double r = sph.x, th = sph.y, ph = sph.z;
+    double st = sin(th), ct = cos(th), sp = sin(ph), cp = cos(ph);
+    k->r0 = r;
+    k->th0 = th;
+    k->ph0 = ph;
+    k->st_cp = st * cp;
+    k->st_sp = st * sp;
+    k->ct = ct;
+    k->ct_cp = ct * cp;
+    k->ct_sp = ct * sp;
+    k->st = st;
+    k->neg_sp = -sp;
+    k->cp = cp;
+    k->r_st = r * st;
+    k->st_tiny = fabs(st) < BH_EPSILON;
+    SchwarzschildMetric m = calculate_schwarzschild_metric(r, &(BlackHoleParams){
+        .schwarzschild_radius = kp->sc.rs});
+    k->g_tt = m.g_tt;
+    k->g_rr = m.g_rr;
+    k->g_hh = m.g_thth;
+    Vector3D p0;
+    spherical_to_cartesian(&sph, &p0);
+    k->p0[0] = p0.x;
+    k->p0[1] = p0.y;
+    k->p0[2] = p0.z;
+    k->use_approx = r > kp->sc.rs_x15;
+}
+
+/* one timed trace-kernel launch on `stream` (the context's own if NULL) */
+static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
+    if (kp->n <= 0) return 0;
+    if (!stream) stream = c->stream;
+    if (c->npend == BHRT_RING && harvest(c) != 0) return -1;
+    int slot = c->next_slot;
+    c->next_slot = (c->next_slot + 1) % BHRT_RING;
+    kp->ctl = c->d_ctl + (size_t)slot * BHRT_CTL_WORDS;
+    HIP_TRY(hipMemsetAsync(kp->ctl, 0, BHRT_CTL_WORDS * sizeof(unsigned long long), stream));
+    pending_t* p = &c->pend[c->npend];
+    p->slot = slot;
+    p->ev0 = c->evpool[2 * c->npend];
+    p->ev1 = c->evpool[2 * c->npend + 1];
+    int e = bhrt_launch_trace(kp, (void*)stream, (void*)p->ev0, (void*)p->ev1);
+    if (e != 0) {
+        set_err("trace kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+        return -1;
+    }
+    c->npend++;
+    return 0;
+}
+
+static int current_device(void) {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return -1;
+    return d;
+}
+
+int bhrt_shard_rows(int H, const bhrt_rows* rows) {
+    if (H <= 0) return 0;
+    if (!rows || rows->num_shards <= 1) return H;
+    if (rows->row_block <= 0 || rows->shard < 0 || rows->shard >= rows->num_shards) return -1;
+    int B = rows->row_block, n = 0;
+    for (long b = rows->shard; b * B < H; b += rows->num_shards) {
+        long hi = (b + 1) * B;
+        n += (int)((hi > H ? H : hi) - b * B);
+    }
+    return n;
+}
+
+static int check_scene(const BlackHoleParams* bh, const SimulationConfig* cfg) {
+    if (!bh || !cfg) {
+        set_err("blackhole and config must not be NULL");
+        return -1;
+    }
+    return 0;
+}
+
+int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                             const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                             const bhrt_rows* rows, IntegrationMethod method, int flags,
+                             const bhrt_frame_soa* out, void* stream) {
+    if (check_scene(bh, cfg) || !cam || !out || W <= 0 || H <= 0) {
+        if (!g_err[0]) set_err("invalid argument");
+        return -1;
+    }
+    int nrows = bhrt_shard_rows(H, rows);
+    if (nrows < 0 || (long)nrows * W > 0x7fffffffL) {
+        set_err("invalid row sharding or frame too large (%d x %d)", W, H);
+        return -1;
+    }
+    int dev = current_device();
+    devctx_t* c = ctx_get(dev);
+    if (!c) return -1;
+    if (out->rgb_r && (!out->rgb_g || !out->rgb_b || !out->result || !out->hit_x || !out->hit_y)) {
+        set_err("rgb output needs rgb_r/g/b, result and hit_x/hit_y");
+        return -1;
+    }
+    bhrt_kparams kp;
+    fill_scene(&kp, bh, dk, cfg, method, flags);
+    fill_camera(&kp, cam, W, H);
+    if (rows && rows->num_shards > 1) kp.cam.rows = *rows;
+    kp.n = nrows * W;
+    kp.out = *out;
+    return launch(c, &kp, (hipStream_t)stream);
+}
+
+int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
+                           const AccretionDiskParams* dk, const SimulationConfig* cfg,
+                           IntegrationMethod method, int flags, const bhrt_frame_soa* out,
+                           void* stream) {
+    if (check_scene(bh, cfg) || !d_rays || !out || n < 0) {
+        if (!g_err[0]) set_err("invalid argument");
+        return -1;
+    }
+    if (out->rgb_r && (!out->rgb_g || !out->rgb_b || !out->result || !out->hit_x || !out->hit_y)) {
+        set_err("rgb output needs rgb_r/g/b, result and hit_x/hit_y");
+        return -1;
+    }
+    devctx_t* c = ctx_get(current_device());
+    if (!c) return -1;
+    if (ensure(&c->d_init, &c->cap_init, (size_t)BHRT_INIT_FIELDS * sizeof(double) * (size_t)n, 0))
+        return -1;
+    bhrt_kparams kp;
+    fill_scene(&kp, bh, dk, cfg, method, flags);
+    kp.src = BHRT_SRC_RAYS;
+    kp.rays = d_rays;
+    kp.init = (double*)c->d_init;
+    kp.n = n;
+    kp.out = *out;
+    return launch(c, &kp, (hipStream_t)stream);
+}
+
+/* ---- host-buffer paths: device SoA block <-> caller SoA ---- */
+static const size_t k_fsize[BHRT_NFIELDS] = {4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
+
+static void** soa_slot(bhrt_frame_soa* s, int f) { return ((void**)s) + f; }
+
+/* carve a device SoA for n rays out of c->d_soa, for the fields `want` requests */
+static int device_soa(devctx_t* c, long n, const bhrt_frame_soa* want_in, bhrt_frame_soa* dev) {
+    bhrt_frame_soa want_buf = *want_in;
+    const bhrt_frame_soa* want = &want_buf;
+    if (want_buf.rgb_r || want_buf.rgb_g || want_buf.rgb_b) { /* the colour pass reads these */
+        want_buf.rgb_r = want_buf.rgb_g = want_buf.rgb_b = (double*)1;
+        if (!want_buf.result) want_buf.result = (int32_t*)1;
+        if (!want_buf.hit_x) want_buf.hit_x = (double*)1;
+        if (!want_buf.hit_y) want_buf.hit_y = (double*)1;
+    }
+    size_t bytes = 0;
+    for (int f = 0; f < BHRT_NFIELDS; f++)
+        if (*soa_slot((bhrt_frame_soa*)want, f)) bytes += ((k_fsize[f] * n + 255) / 256) * 256;
+    if (ensure(&c->d_soa, &c->cap_soa, bytes ? bytes : 256, 0)) return -1;
+    memset(dev, 0, sizeof *dev);
+    char* p = (char*)c->d_soa;
+    for (int f = 0; f < BHRT_NFIELDS; f++)
+        if (*soa_slot((bhrt_frame_soa*)want, f)) {
+            *soa_slot(dev, f) = p;
+            p += ((k_fsize[f] * n + 255) / 256) * 256;
+        }
+    return 0;
+}
+
+typedef struct {
+    devctx_t* c;
+    bhrt_frame_soa dev;
+    long n;
+} shard_job;
+
+/* copy a finished device SoA back into `host` at element offsets given by map(j) */
+static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_rows* rows) {
+    devctx_t* c = j->c;
+    HIP_TRY(hipSetDevice(c->device));
+    size_t bytes = 0;
+    for (int f = 0; f < BHRT_NFIELDS; f++)
+        if (*soa_slot(&j->dev, f)) bytes += k_fsize[f] * (size_t)j->n;
+    if (ensure(&c->h_stage, &c->cap_stage, bytes ? bytes : 64, 1)) return -1;
+    char* stage = (char*)c->h_stage;
+    size_t off = 0;
+    for (int f = 0; f < BHRT_NFIELDS; f++) {
+        void* src = *soa_slot(&j->dev, f);
+        if (!src) continue;
+        HIP_TRY(hipMemcpyAsync(stage + off, src, k_fsize[f] * (size_t)j->n,
+                               hipMemcpyDeviceToHost, c->stream));
+        off += k_fsize[f] * (size_t)j->n;
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    off = 0;
+    for (int f = 0; f < BHRT_NFIELDS; f++) {
+        void* src = *soa_slot(&j->dev, f);
+        if (!src) continue;
+        char* dst = (char*)*soa_slot((bhrt_frame_soa*)host, f);
+        size_t fs = k_fsize[f];
+        if (!rows || rows->num_shards <= 1) {
+            memcpy(dst, stage + off, fs * (size_t)j->n);
+        } else { /* un-permute cyclic row blocks */
+            long nrow = j->n / W;
+            for (long r = 0; r < nrow; r++) {
+                long B = rows->row_block;
+                long g = ((r / B) * rows->num_shards + rows->shard) * B + r % B;
+                memcpy(dst + fs * (size_t)(g * W), stage + off + fs * (size_t)(r * W), fs * (size_t)W);
+            }
+        }
+        off += fs * (size_t)j->n;
+    }
+    return 0;
+}
+
+int bhrt_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                      const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                      IntegrationMethod method, int flags, const bhrt_frame_soa* host) {
+    if (check_scene(bh, cfg) || !cam || !host || W <= 0 || H <= 0) {
+        if (!g_err[0]) set_err("invalid argument");
+        return -1;
+    }
+    int ndev = bhrt_device_count();
+    if (ndev <= 0) {
+        set_err("no HIP device available (libbhrt has no CPU path)");
+        return -1;
+    }
+    int block = 8;
+    if (ndev > 1 && H < ndev * block) ndev = 1;
+    shard_job jobs[BHRT_MAX_DEV];
+    bhrt_rows rows[BHRT_MAX_DEV];
+    for (int d = 0; d < ndev; d++) {
+        rows[d].row_block = block;
+        rows[d].shard = d;
+        rows[d].num_shards = ndev;
+        devctx_t* c = ctx_get(d);
+        if (!c) return -1;
+        HIP_TRY(hipSetDevice(d));
+        jobs[d].c = c;
+        jobs[d].n = (long)bhrt_shard_rows(H, &rows[d]) * W;
+        if (device_soa(c, jobs[d].n, host, &jobs[d].dev)) return -1;
+        if (bhrt_render_frame_device(bh, dk, cfg, cam, W, H, &rows[d], method, flags,
+                                     &jobs[d].dev, c->stream))
+            return -1;
+    }
+    for (int d = 0; d < ndev; d++)
+        if (readback(&jobs[d], host, W, ndev > 1 ? &rows[d] : NULL)) return -1;
+    return 0;
+}
+
+int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
+                    const AccretionDiskParams* dk, const SimulationConfig* cfg,
+                    IntegrationMethod method, int flags, const bhrt_frame_soa* host) {
+    if (check_scene(bh, cfg) || !rays || !host || n < 0) {
+        if (!g_err[0]) set_err("invalid argument");
+        return -1;
+    }
+    if (n == 0) return 0;
+    int ndev = bhrt_device_count();
+    if (ndev <= 0) {
+        set_err("no HIP device available (libbhrt has no CPU path)");
+        return -1;
+    }
+    if (n < 4096 * ndev) ndev = 1; /* small batches: one device, one launch */
+    shard_job jobs[BHRT_MAX_DEV];
+    long base[BHRT_MAX_DEV + 1];
+    for (int d = 0; d <= ndev; d++) base[d] = (long)n * d / ndev;
+    for (int d = 0; d < ndev; d++) {
+        devctx_t* c = ctx_get(d);
+        if (!c) return -1;
+        HIP_TRY(hipSetDevice(d));
+        long m = base[d + 1] - base[d];
+        jobs[d].c = c;
+        jobs[d].n = m;
+        if (ensure(&c->d_rays, &c->cap_rays, (size_t)m * sizeof(Ray), 0)) return -1;
+        if (device_soa(c, m, host, &jobs[d].dev)) return -1;
+        HIP_TRY(hipMemcpyAsync(c->d_rays, rays + base[d], (size_t)m * sizeof(Ray),
+                               hipMemcpyHostToDevice, c->stream));
+        if (bhrt_trace_rays_device((const Ray*)c->d_rays, (int)m, bh, dk, cfg, method, flags,
+                                   &jobs[d].dev, c->stream))
+            return -1;
+    }
+    for (int d = 0; d < ndev; d++) {
+        bhrt_frame_soa h = *host;
+        for (int f = 0; f < BHRT_NFIELDS; f++) {
+            char** s = (char**)soa_slot(&h, f);
+            if (*s) *s += k_fsize[f] * (size_t)base[d];
+        }
+        if (readback(&jobs[d], &h, 0, NULL)) return -1;
+    }
+    return 0;
+}
+
+/* ======================================================================================= */
+/* drop-in ray tracing entry points                                                        */
+/* ======================================================================================= */
+
+/* trace rays into RayTraceHit[], writing exactly the fields trace_ray writes
+ * (raytracer.c:299-333, 728-753) */
+static int trace_into_hits(const Ray* rays, int n, const BlackHoleParams* bh,
+                           const AccretionDiskParams* dk, const SimulationConfig* cfg,
+                           RayTraceHit* hits) {
+    size_t per = 2 * sizeof(int32_t) + 8 * sizeof(double);
+    char* buf = (char*)malloc(per * (size_t)n);
+    if (!buf) {
+        set_err("host allocation failed");
+        return -1;
+    }
+    bhrt_frame_soa s;
+    memset(&s, 0, sizeof s);
+    s.result = (int32_t*)buf;
+    s.steps = s.result + n;
+    s.hit_x = (double*)(s.steps + n);
+    s.hit_y = s.hit_x + n;
+    s.hit_z = s.hit_y + n;
+    s.distance = s.hit_z + n;
+    s.time_dilation = s.distance + n;
+    s.sky_x = s.time_dilation + n;
+    s.sky_y = s.sky_x + n;
+    s.sky_z = s.sky_y + n;
+    int rc = bhrt_trace_rays(rays, n, bh, dk, cfg, INTEGRATOR_RK4, 0, &s);
+    if (rc == 0) {
+        for (int i = 0; i < n; i++) {
+            RayTraceHit* h = &hits[i];
+            h->result = (RayTraceResult)s.result[i];
+            h->steps = s.steps[i];
+            h->hit_position.x = s.hit_x[i];
+            h->hit_position.y = s.hit_y[i];
+            h->hit_position.z = s.hit_z[i];
+            h->distance = s.distance[i];
+            h->time_dilation = s.time_dilation[i];
+            if (h->result == RAY_MAX_DISTANCE) {
+                h->sky_direction.x = s.sky_x[i];
+                h->sky_direction.y = s.sky_y[i];
+                h->sky_direction.z = s.sky_z[i];
+            }
+        }
+    }
+    free(buf);
+    return rc;
+}
+
+RayTraceResult trace_ray(const Ray* ray, const BlackHoleParams* bh,
+                         const AccretionDiskParams* dk, const SimulationConfig* cfg,
+                         RayTraceHit* hit) {
+    if (!ray || check_scene(bh, cfg)) return RAY_ERROR;
+    RayTraceHit tmp;
+    RayTraceHit* h = hit ? hit : &tmp;
+    if (trace_into_hits(ray, 1, bh, dk, cfg, h) != 0) {
+        if (hit) hit->result = RAY_ERROR;
+        return RAY_ERROR;
+    }
+    return h->result;
+}
+
+int trace_rays_batch(const Ray* rays, int n, const BlackHoleParams* bh,
+                     const AccretionDiskParams* dk, const SimulationConfig* cfg,
+                     RayTraceHit* hits, int num_threads) {
+    (void)num_threads;
+    if (!rays || !bh || !hits || n <= 0) return -1; /* raytracer.c:791-793 */
+    if (!cfg) {
+        set_err("config must not be NULL");
+        return -1;
+    }
+    if (trace_into_hits(rays, n, bh, dk, cfg, hits) != 0) {
+        for (int i = 0; i < n; i++) hits[i].result = RAY_ERROR;
+        return -1;
+    }
+    return 0;
+}
+
+RayTraceResult integrate_photon_path(const Vector4D* position, const Vector3D* direction,
+                                     const BlackHoleParams* bh, const SimulationConfig* cfg,
+                                     IntegrationMethod method, Vector3D* path, int max_positions,
+                                     int* num_positions, RayTraceHit* hit) {
+    if (!position || !direction || check_scene(bh, cfg)) return RAY_ERROR;
+    int dev = current_device();
+    devctx_t* c = ctx_get(dev);
+    if (!c) return RAY_ERROR;
+    const int record = path != NULL && num_positions != NULL &&
+                       (max_positions > 0 || *num_positions < max_positions);
+    const int num_in = (path && max_positions <= 0 && num_positions) ? *num_positions : 0;
+    size_t path_bytes = record && max_positions > 0 ? (size_t)max_positions * sizeof(Vector3D) : 0;
+    /* layout: [hit SoA: 2 ints + 8 doubles][num][path] */
+    size_t need = 128 + 64 + path_bytes;
+    if (ensure(&c->d_rays, &c->cap_rays, need, 0)) return RAY_ERROR;
+    char* d = (char*)c->d_rays;
+    bhrt_frame_soa s;
+    memset(&s, 0, sizeof s);
+    s.result = (int32_t*)d;
+    s.steps = (int32_t*)(d + 8);
+    s.hit_x = (double*)(d + 16);
+    s.hit_y = s.hit_x + 1;
+    s.hit_z = s.hit_x + 2;
+    s.distance = s.hit_x + 3;
+    s.time_dilation = s.hit_x + 4;
+    s.sky_x = s.hit_x + 5;
+    s.sky_y = s.hit_x + 6;
+    s.sky_z = s.hit_x + 7;
+    int* d_num = (int*)(d + 128);
+    Vector3D* d_path = path_bytes ? (Vector3D*)(d + 192) : NULL;
+    bhrt_kparams kp;
+    fill_scene(&kp, bh, NULL, cfg, method, 0);
+    kp.src = BHRT_SRC_RAYS;
+    kp.n = 1;
+    kp.out = s;
+    double o4[4] = {position->t, position->x, position->y, position->z};
+    double d3[3] = {direction->x, direction->y, direction->z};
+    if (bhrt_launch_path(&kp, o4, d3, d_path, max_positions, d_num, num_in, c->stream) != 0) {
+        set_err("path kernel launch failed");
+        return RAY_ERROR;
+    }
+    char h[128 + 64];
+    if (hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        set_err("path kernel failed: %s", hipGetErrorString(hipGetLastError()));
+        return RAY_ERROR;
+    }
+    int num = *(int*)(h + 128);
+    if (d_path && num > 0) {
+        int cnt = num < max_positions ? num : max_positions;
+        if (hipMemcpy(path, d_path, (size_t)cnt * sizeof(Vector3D), hipMemcpyDeviceToHost) !=
+            hipSuccess) {
+            set_err("path readback failed");
+            return RAY_ERROR;
+        }
+    }
+    if (path && num_positions && max_positions > 0) *num_positions = num;
+    RayTraceResult res = (RayTraceResult)(*(int32_t*)h);
+    if (hit) {
+        const double* v = (const double*)(h + 16);
+        hit->result = res;
+        hit->steps = *(int32_t*)(h + 8);
+        hit->hit_position.x = v[0];
+        hit->hit_position.y = v[1];
+        hit->hit_position.z = v[2];
+        hit->distance = v[3];
+        hit->time_dilation = v[4];
+        if (res == RAY_MAX_DISTANCE) {
+            hit->sky_direction.x = v[5];
+            hit->sky_direction.y = v[6];
+            hit->sky_direction.z = v[7];
+        }
+    }
+    return res;
+}
+
+/* raytracer.c:868-932 */
+static void jitter(int sample, int spp, JitterMethod jm, double strength, double* ox,
+                   double* oy) {
+    *ox = 0.5;
+    *oy = 0.5;
+    switch (jm) {
+    case JITTER_REGULAR_GRID: {
+        int g = (int)sqrt((double)spp);
+        int x = sample % g, y = sample / g;
+        *ox = (x + 0.5) / g;
+        *oy = (y + 0.5) / g;
+    } break;
+    case JITTER_RANDOM:
+        *ox = (double)rand() / RAND_MAX;
+        *oy = (double)rand() / RAND_MAX;
+        break;
+    case JITTER_HALTON:
+    case JITTER_BLUE_NOISE:
+        *ox = halton_sequence(sample, 2);
+        *oy = halton_sequence(sample, 3);
+        break;
+    default: break;
+    }
+    if (strength != 1.0) {
+        *ox = 0.5 + (*ox - 0.5) * strength;
+        *oy = 0.5 + (*oy - 0.5) * strength;
+    }
+}
+
+/* raytracer.c:1044-1167: all samples of the pixel are traced in one GPU launch. Disk
+ * samples take the frame colour contract's disk colour (the reference reads the never
+ * written RayTraceHit.color there). */
+RayTraceResult trace_pixel(int px, int py, int W, int H, const Vector3D* cam_pos,
+                           const Vector3D* cam_dir, const Vector3D* cam_up, double fov,
+                           const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                           const SimulationConfig* cfg, const SupersamplingParams* ss,
+                           const AdaptiveSamplingParams* as, double color_out[3]) {
+    color_out[0] = color_out[1] = color_out[2] = 0.0;
+    int samples = ss ? ss->samples_per_pixel : 1;
+    if (as && as->enable_adaptive) { /* :1076-1093, edge_factor fixed at 1.0 */
+        samples = as->min_samples;
+        samples += (int)((as->max_samples - as->min_samples) * 1.0);
+        if (samples > as->max_samples) samples = as->max_samples;
+    }
+    RayTraceResult result = RAY_BACKGROUND;
+    if (samples > 0) {
+        if (!cam_pos || !cam_dir || !cam_up || check_scene(bh, cfg)) return RAY_ERROR;
+        Ray* rays = (Ray*)malloc(sizeof(Ray) * (size_t)samples);
+        double* rgb = (double*)malloc(sizeof(double) * 3 * (size_t)samples);
+        int32_t* res = (int32_t*)malloc(sizeof(int32_t) * (size_t)samples);
+        if (!rays || !rgb || !res) {
+            free(rays); free(rgb); free(res);
+            return RAY_ERROR;
+        }
+        bhrt_camera cam = {*cam_pos, *cam_dir, *cam_up, fov};
+        bhrt_kparams basis;
+        fill_scene(&basis, bh, dk, cfg, INTEGRATOR_RK4, 0);
+        fill_camera(&basis, &cam, W, H);
+        for (int s = 0; s < samples; s++) {
+            double ox = 0.5, oy = 0.5;
+            if (ss && ss->samples_per_pixel > 1)
+                jitter(s, ss->samples_per_pixel, ss->jitter_method, ss->jitter_strength, &ox, &oy);
+            double ndcx = (2.0 * ((px + ox) / W) - 1.0) * basis.cam.plane_w;
+            double ndcy = (1.0 - 2.0 * ((py + oy) / H)) * basis.cam.plane_h;
+            Vector3D f = {basis.cam.fwd[0], basis.cam.fwd[1], basis.cam.fwd[2]};
+            Vector3D r = {basis.cam.right[0], basis.cam.right[1], basis.cam.right[2]};
+            Vector3D u = {basis.cam.up[0], basis.cam.up[1], basis.cam.up[2]};
+            Vector3D d = vector3D_add(f, vector3D_scale(r, ndcx));
+            d = vector3D_add(d, vector3D_scale(u, ndcy));
+            rays[s].origin = *cam_pos;
+            rays[s].direction = vector3D_normalize(d);
+        }
+        bhrt_frame_soa soa;
+        memset(&soa, 0, sizeof soa);
+        soa.result = res;
+        soa.rgb_r = rgb;
+        soa.rgb_g = rgb + samples;
+        soa.rgb_b = rgb + 2 * samples;
+        int rc = bhrt_trace_rays(rays, samples, bh, dk, cfg, INTEGRATOR_RK4, 0, &soa);
+        if (rc == 0) {
+            result = (RayTraceResult)res[0];
+            for (int s = 0; s < samples; s++) {
+                color_out[0] += soa.rgb_r[s];
+                color_out[1] += soa.rgb_g[s];
+                color_out[2] += soa.rgb_b[s];
+            }
+        }
+        free(rays); free(rgb); free(res);
+        if (rc != 0) return RAY_ERROR;
+    }
+    color_out[0] /= samples;
+    color_out[1] /= samples;
+    color_out[2] /= samples;
+    return result;
+}
+
+/* ======================================================================================= */
+/* scalar helpers of the ray path (host side of the drop-in)                                */
+/* ======================================================================================= */
+int check_disk_intersection(const Vector3D* p, const Vector3D* v, const Vector3D* n,
+                            const AccretionDiskParams* disk, Vector3D* q) {
+    double den = vector3D_dot(*v, *n);
+    if (fabs(den) < BH_EPSILON) return 0;
+    double t = -(vector3D_dot(*p, *n)) / den;
+    if (t < 0.0) return 0;
+    *q = vector3D_add(*p, vector3D_scale(*v, t));
+    double r = sqrt(q->x * q->x + q->y * q->y);
+    return r >= disk->inner_radius && r <= disk->outer_radius;
+}
+
+void temperature_to_rgb(double T, double rgb[3]) {
+    T = clamp(T, 1000.0, 40000.0);
+    double t = (T - 1000.0) / (40000.0 - 1000.0);
+    rgb[0] = t < 0.5 ? t * 2.0 : 1.0;
+    rgb[1] = t < 0.25 ? 0.0 : (t < 0.75 ? (t - 0.25) * 2.0 : 1.0);
+    rgb[2] = t < 0.5 ? 0.0 : (t - 0.5) * 2.0;
+    double br = 0.2 + 0.8 * (t * t);
+    rgb[0] *= br;
+    rgb[1] *= br;
+    rgb[2] *= br;
+}
+
+void calculate_disk_temperature(const Vector3D* p, const BlackHoleParams* bh,
+                                const AccretionDiskParams* disk, double* T, double color[3]) {
+    (void)bh;
+    double r = sqrt(p->x * p->x + p->y * p->y);
+    double nr = clamp((r - disk->inner_radius) / (disk->outer_radius - disk->inner_radius), 0.0, 1.0);
+    *T = disk->temperature_scale * (2000.0 + 18000.0 * pow(1.0 - nr, 0.75));
+    temperature_to_rgb(*T, color);
+}
+
+double calculate_time_dilation(double r, const BlackHoleParams* bh) {
+    return 1.0 / sqrt(1.0 - bh->schwarzschild_radius / r);
+}
+
+void apply_relativistic_effects(const Vector3D* p, const Vector3D* v, const BlackHoleParams* bh,
+                                double c[3], double* dop_out) {
+    double r = sqrt(p->x * p->x + p->y * p->y);
+    double phi = atan2(p->y, p->x);
+    Vector3D tangent = {-sin(phi), cos(phi), 0.0};
+    double dop = 1.0 + vector3D_dot(*v, tangent) * 0.5;
+    double z = dop / calculate_time_dilation(r, bh);
+    if (z < 1.0) {
+        c[2] *= z;
+        c[0] = fmin(1.0, c[0] * (2.0 - z));
+    } else {
+        c[0] *= 2.0 - z;
+        c[2] = fmin(1.0, c[2] * z);
+    }
+    double beam = pow(dop, 4);
+    c[0] = clamp(c[0] * beam, 0.0, 1.0);
+    c[1] = clamp(c[1] * beam, 0.0, 1.0);
+    c[2] = clamp(c[2] * beam, 0.0, 1.0);
+    if (dop_out) *dop_out = dop;
+}
+
+void generate_gpu_shader_params(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                                double observer_distance, double fov, GPUShaderParams* p) {
+    if (!bh || !p) return;
+    p->mass = bh->mass;
+    p->spin = bh->spin;
+    p->schwarzschild_radius = 2.0 * bh->mass;
+    p->observer_distance = observer_distance;
+    p->fov = fov;
+    if (dk) {
+        p->disk_inner_radius = dk->inner_radius;
+        p->disk_outer_radius = dk->outer_radius;
+        p->disk_temp_scale = dk->temperature_scale;
+    } else {
+        p->disk_inner_radius = 3.0 * p->schwarzschild_radius;
+        p->disk_outer_radius = 20.0 * p->schwarzschild_radius;
+        p->disk_temp_scale = 1.0;
+    }
+}
+
+double halton_sequence(int index, int base) {
+    double result = 0.0, f = 1.0;
+    for (; index > 0; index /= base) {
+        f /= base;
+        result += f * (index % base);
+    }
+    return result;
+}
+
+SchwarzschildMetric calculate_schwarzschild_metric(double r, const BlackHoleParams* bh) {
+    SchwarzschildMetric m;
+    double rs = bh->schwarzschild_radius;
+    if (r <= rs + BH_EPSILON) r = rs + BH_EPSILON;
+    m.g_tt = -(1.0 - rs / r);
+    m.g_rr = 1.0 / (1.0 - rs / r);
+    m.g_thth = r * r;
+    m.g_phph = r * r; /* r*r*sin^2(pi/2), sin(pi/2) == 1.0 in double */
+    return m;
+}
+
+void cartesian_to_spherical(const Vector3D* c, Vector3D* s) {
+    double r = sqrt(c->x * c->x + c->y * c->y + c->z * c->z);
+    double th = r > BH_EPSILON ? acos(c->z / r) : 0.0;
+    double ph = atan2(c->y, c->x);
+    if (ph < 0.0) ph += BH_TWO_PI;
+    s->x = r;
+    s->y = th;
+    s->z = ph;
+}
+
+void spherical_to_cartesian(const Vector3D* s, Vector3D* c) {
+    c->x = s->x * sin(s->y) * cos(s->z);
+    c->y = s->x * sin(s->y) * sin(s->z);
+    c->z = s->x * cos(s->y);
+}
+
+double get_isco_radius(const BlackHoleParams* bh) {
+    double M = bh->mass, a = bh->spin * M;
+    if (bh->spin == 0.0) return 6.0 * M;
+    double third = 1.0 / 3.0;
+    double z1 = 1.0 + pow(1.0 - a * a / (M * M), third) *
+                          (pow(1.0 + a / (M), third) + pow(1.0 - a / (M), third));
+    double z2 = sqrt(3.0 * a * a / (M * M) + z1 * z1);
+    return M * (3.0 + z2 - sqrt((3.0 - z1) * (3.0 + z1 + 2.0 * z2)));
+}
+
+void initialize_black_hole_params(BlackHoleParams* bh, double mass, double spin, double charge) {
+    bh->mass = mass;
+    bh->spin = spin;
+    bh->charge = charge;
+    bh->schwarzschild_radius = 2.0 * mass; /* every branch: spacetime.c:338,348,358 */
+    bh->ergosphere_radius = 2.0 * mass;
+    if (spin == 0.0 && charge == 0.0) {
+        bh->r_plus = 2.0 * mass;
+        bh->r_minus = 0.0;
+    } else {
+        double a = spin * mass;
+        double q2 = (spin > 0.0 && charge == 0.0) ? 0.0 : charge * charge;
+        double s = q2 == 0.0 ? sqrt(mass * mass - a * a) : sqrt(mass * mass - a * a - q2);
+        bh->r_plus = mass + s;
+        bh->r_minus = mass - s;
+    }
+    bh->isco_radius = get_isco_radius(bh);
+}
+
+/* ---- generic host integrators (math_util.c:162-457; debug printing not reproduced) ---- */
+void rk4_integrate(ODEFunction f, double* y, int n, double t, double h, void* params) {
+    double* w = (double*)malloc(sizeof(double) * 5 * (size_t)(n > 0 ? n : 1));
+    if (!w) return;
+    double *k1 = w, *k2 = w + n, *k3 = w + 2 * n, *k4 = w + 3 * n, *yt = w + 4 * n;
+    f(t, y, k1, params);
+    for (int i = 0; i < n; i++) yt[i] = y[i] + 0.5 * h * k1[i];
+    f(t + 0.5 * h, yt, k2, params);
+    for (int i = 0; i < n; i++) yt[i] = y[i] + 0.5 * h * k2[i];
+    f(t + 0.5 * h, yt, k3, params);
+    for (int i = 0; i < n; i++) yt[i] = y[i] + h * k3[i];
+    f(t + h, yt, k4, params);
+    for (int i = 0; i < n; i++) y[i] += h * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]) / 6.0;
+    free(w);
+}
+
+int rkf45_integrate(ODEFunction f, double y[], int n, double* t, double h, double* h_next,
+                    double eps_rel, void* params) {
+    static const double A[6] = {0.0, 1.0 / 4.0, 3.0 / 8.0, 12.0 / 13.0, 1.0, 1.0 / 2.0};
+    static const double B[6][5] = {
+        {0, 0, 0, 0, 0},
+        {1.0 / 4.0, 0, 0, 0, 0},
+        {3.0 / 32.0, 9.0 / 32.0, 0, 0, 0},
+        {1932.0 / 2197.0, -7200.0 / 2197.0, 7296.0 / 2197.0, 0, 0},
+        {439.0 / 216.0, -8.0, 3680.0 / 513.0, -845.0 / 4104.0, 0},
+        {-8.0 / 27.0, 2.0, -3544.0 / 2565.0, 1859.0 / 4104.0, -11.0 / 40.0}};
+    static const double C4[6] = {25.0 / 216.0, 0, 1408.0 / 2565.0, 2197.0 / 4104.0, -1.0 / 5.0, 0};
+    static const double C5[6] = {16.0 / 135.0, 0, 6656.0 / 12825.0, 28561.0 / 56430.0,
+                                 -9.0 / 50.0, 2.0 / 55.0};
+    double* w = (double*)malloc(sizeof(double) * 9 * (size_t)(n > 0 ? n : 1));
+    if (!w) return 1;
+    double* k[6];
+    for (int s = 0; s < 6; s++) k[s] = w + s * n;
+    double *yt = w + 6 * n, *y4 = w + 7 * n, *y5 = w + 8 * n;
+    int rc = 1;
+    f(*t, y, k[0], params);
+    for (int i = 0; i < n; i++)
+        if (isnan(k[0][i]) || isinf(k[0][i])) goto out;
+    for (int s = 1; s < 6; s++) {
+        for (int i = 0; i < n; i++) {
+            /* same left-to-right sums as the unrolled reference: h*b21*k1 for stage 2,
+             * h*(b31*k1 + b32*k2 + ...) afterwards */
+            double acc;
+            if (s == 1) {
+                yt[i] = y[i] + h * B[1][0] * k[0][i];
+                continue;
+            }
+            acc = B[s][0] * k[0][i];
+            for (int j = 1; j < s; j++) acc = acc + B[s][j] * k[j][i];
+            yt[i] = y[i] + h * acc;
+        }
+        f(*t + h * A[s], yt, k[s], params);
+    }
+    double max_error = 0.0;
+    for (int i = 0; i < n; i++) {
+        y4[i] = y[i] + h * (C4[0] * k[0][i] + C4[2] * k[2][i] + C4[3] * k[3][i] + C4[4] * k[4][i]);
+        y5[i] = y[i] + h * (C5[0] * k[0][i] + C5[2] * k[2][i] + C5[3] * k[3][i] +
+                            C5[4] * k[4][i] + C5[5] * k[5][i]);
+        double scale = fmax(fabs(y[i]), fabs(y5[i]));
+        if (scale < BH_EPSILON) scale = BH_EPSILON;
+        max_error = fmax(max_error, fabs(y5[i] - y4[i]) / scale);
+    }
+    double ratio = max_error / eps_rel;
+    if (ratio <= 1.0) {
+        double scale = ratio == 0.0 ? 10.0 : fmax(0.2, fmin(10.0, 0.9 * pow(ratio, -0.2)));
+        for (int i = 0; i < n; i++) y[i] = y5[i];
+        *t = *t + h;
+        *h_next = h * scale;
+        rc = 0;
+    } else {
+        *h_next = h * fmax(0.2, fmin(10.0, 0.9 * pow(ratio, -0.25)));
+    }
+out:
+    free(w);
+    return rc;
+}
+
+/* ======================================================================================= */
+/* context API (src/blackhole_api.c)                                                       */
+/* ======================================================================================= */
+struct BHContext_t {
+    BlackHoleParams blackhole;
+    AccretionDiskParams disk;
+    SimulationConfig config;
+    int disk_enabled;
+};
+
+BHContextHandle bh_initialize(void) { /* blackhole_api.c:52-80 */
+    BHContextHandle c = (BHContextHandle)calloc(1, sizeof(struct BHContext_t));
+    if (!c) return NULL;
+    c->blackhole.mass = 1.0;
+    c->blackhole.schwarzschild_radius = 2.0;
+    c->disk.inner_radius = 6.0;
+    c->disk.outer_radius = 20.0;
+    c->disk.temperature_scale = 1.0;
+    c->disk.density_scale = 1.0;
+    c->config.time_step = 0.1;
+    c->config.max_ray_distance = 100.0;
+    c->config.max_integration_steps = 1000;
+    c->config.tolerance = 1.0e-6;
+    return c;
+}
+
+void bh_shutdown(BHContextHandle c) { free(c); }
+
+double blackhole_get_mass(BHContextHandle c) { return c ? c->blackhole.mass : 0.0; }
+
+void bh_calculate_orbital_velocity(BHContextHandle c, double r, double* v_phi) {
+    if (!c || !v_phi || r <= 0) return;
+    *v_phi = sqrt(blackhole_get_mass(c) / r);
+}
+
+BHErrorCode bh_configure_black_hole(BHContextHandle c, double mass, double spin, double charge) {
+    if (!c || mass <= 0.0 || spin < 0.0 || spin > 1.0) return BH_ERROR_INVALID_PARAMETER;
+    initialize_black_hole_params(&c->blackhole, mass, spin, charge);
+    return BH_SUCCESS;
+}
+
+BHErrorCode bh_configure_accretion_disk(BHContextHandle c, double inner, double outer,
+                                        double tscale, double density) {
+    if (!c || inner <= 0.0 || outer <= inner || tscale <= 0.0 || density <= 0.0)
+        return BH_ERROR_INVALID_PARAMETER;
+    c->disk.inner_radius = inner;
+    c->disk.outer_radius = outer;
+    c->disk.temperature_scale = tscale;
+    c->disk.density_scale = density;
+    c->disk_enabled = 1;
+    return BH_SUCCESS;
+}
+
+BHErrorCode bh_configure_simulation(BHContextHandle c, double dt, double max_dist, int max_steps,
+                                    double tol) {
+    if (!c || dt <= 0.0 || max_dist <= 0.0 || max_steps <= 0 || tol <= 0.0)
+        return BH_ERROR_INVALID_PARAMETER;
+    c->config.time_step = dt;
+    c->config.max_ray_distance = max_dist;
+    c->config.max_integration_steps = max_steps;
+    c->config.tolerance = tol;
+    return BH_SUCCESS;
+}
+
+BHErrorCode bh_trace_ray(BHContextHandle c, const double origin[3], const double direction[3],
+                         RayTraceHit* hit) {
+    if (!c || !origin || !direction || !hit) return BH_ERROR_INVALID_PARAMETER;
+    Ray ray;
+    ray.origin.x = origin[0];
+    ray.origin.y = origin[1];
+    ray.origin.z = origin[2];
+    Vector3D d = {direction[0], direction[1], direction[2]};
+    ray.direction = vector3D_normalize(d); /* blackhole_api.c:203-204 */
+    RayTraceResult r = trace_ray(&ray, &c->blackhole, c->disk_enabled ? &c->disk : NULL,
+                                 &c->config, hit);
+    return r == RAY_ERROR ? BH_ERROR_SIMULATION : BH_SUCCESS;
+}
+
+BHErrorCode bh_trace_rays_batch(BHContextHandle c, const Ray* rays, RayTraceHit* hits, int count) {
+    if (!c || !rays || !hits || count <= 0) return BH_ERROR_INVALID_PARAMETER;
+    if (trace_rays_batch(rays, count, &c->blackhole, c->disk_enabled ? &c->disk : NULL,
+                         &c->config, hits, 0) != 0)
+        return BH_ERROR_SIMULATION;
+    for (int i = 0; i < count; i++)
+        if (hits[i].result == RAY_ERROR) return BH_ERROR_SIMULATION;
+    return BH_SUCCESS;
+}
+
+BHErrorCode bh_calculate_time_dilation(BHContextHandle c, const double p1[3], const double p2[3],
+                                       double* ratio) {
+    if (!c || !p1 || !p2 || !ratio) return BH_ERROR_INVALID_PARAMETER;
+    double r1 = sqrt(p1[0] * p1[0] + p1[1] * p1[1] + p1[2] * p1[2]);
+    double r2 = sqrt(p2[0] * p2[0] + p2[1] * p2[1] + p2[2] * p2[2]);
+    *ratio = calculate_time_dilation(r1, &c->blackhole) / calculate_time_dilation(r2, &c->blackhole);
+    return BH_SUCCESS;
+}
+
+void bh_get_version(int* major, int* minor, int* patch) {
+    if (major) *major = BLACKHOLE_API_VERSION_MAJOR;
+    if (minor) *minor = BLACKHOLE_API_VERSION_MINOR;
+    if (patch) *patch = BLACKHOLE_API_VERSION_PATCH;
+}
+
+/* blackhole_api.c:495-608: packs a float parameter block for a shader */
+BHErrorCode bh_generate_shader_data(void* context, const float pos[3], const float dir[3],
+                                    const float up[3], int width, int height, float fov,
+                                    int enable_doppler, int enable_redshift, int show_disk,
+                                    float* out) {
+    if (!context || !pos || !dir || !up || !out) return BH_ERROR_INVALID_PARAMETER;
+    BHContextHandle c = (BHContextHandle)context;
+    struct {
+        float mass, spin, schwarzschild_radius, r_isco, r_horizon;
+        float disk_inner_radius, disk_outer_radius, disk_temp_scale, disk_density_scale;
+        float observer_pos[3], observer_dir[3], up_vector[3];
+        float fov, aspect_ratio;
+        int enable_doppler, enable_redshift, show_disk;
+        int max_steps;
+        float step_size, tolerance, max_distance;
+        float padding[4];
+    } p;
+    p.mass = (float)c->blackhole.mass;
+    p.spin = (float)c->blackhole.spin;
+    p.schwarzschild_radius = (float)c->blackhole.schwarzschild_radius;
+    p.r_isco = (float)c->blackhole.isco_radius;
+    p.r_horizon = (float)c->blackhole.r_plus;
+    int disk_on = show_disk && c->disk_enabled;
+    p.disk_inner_radius = disk_on ? (float)c->disk.inner_radius : 1000.0f;
+    p.disk_outer_radius = disk_on ? (float)c->disk.outer_radius : 100.0f;
+    p.disk_temp_scale = disk_on ? (float)c->disk.temperature_scale : 0.0f;
+    p.disk_density_scale = disk_on ? (float)c->disk.density_scale : 0.0f;
+    memcpy(p.observer_pos, pos, sizeof p.observer_pos);
+    memcpy(p.observer_dir, dir, sizeof p.observer_dir);
+    memcpy(p.up_vector, up, sizeof p.up_vector);
+    p.fov = fov * (float)BH_PI / 180.0f;
+    p.aspect_ratio = (float)width / (float)height;
+    p.enable_doppler = enable_doppler;
+    p.enable_redshift = enable_redshift;
+    p.show_disk = disk_on;
+    p.max_steps = c->config.max_integration_steps;
+    p.step_size = (float)c->config.time_step;
+    p.tolerance = (float)c->config.tolerance;
+    p.max_distance = (float)c->config.max_ray_distance;
+    memset(p.padding, 0, sizeof p.padding);
+    memcpy(out, &p, sizeof p);
+    return BH_SUCCESS;
+}

@@ -1,0 +1,78 @@
+/*
+ * bhrt_kernel.h -- launch parameters shared by the C host layer (bhrt_api.c) and the HIP
+ * kernels (geodesic.hip). Plain C, passed by value as the kernel argument block, so every
+ * field is wave-uniform and read through the scalar unit.
+ *
+ * Everything that is the same for all rays of a launch is computed ONCE on the host with
+ * the same IEEE operations the reference performs inline (so identical rounding):
+ *   - the scene constants (rs*1.5, dt*0.001, ...);
+ *   - for a camera frame, the spherical coordinates of the shared origin (glibc acos /
+ *     atan2 / sin / cos, exactly the reference's values) and the metric there.
+ */
+#ifndef BHRT_KERNEL_H
+#define BHRT_KERNEL_H
+
+#include "../../include/bhrt_api.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { BHRT_SRC_RAYS = 0, BHRT_SRC_CAMERA = 1 };
+enum { BHRT_NUM_COUNTERS = 5 }; /* rays, iterations, stages full/far/kerr */
+enum { BHRT_INIT_FIELDS = 15 }; /* y0..y5, y6, y7, dx, dy, dz, px, py, pz, far_ok */
+
+typedef struct {
+    /* scene constants (raytracer.c:65-130, 465, 556-571, 652-659; spacetime.c:22) */
+    double M, rs, two_m;
+    double rs_x1_5, rs_x1_05, rs_x2_5, rs_x5, rs_x15, rs_eps;
+    double h_2_5, h_5, h_15, h_far;
+    double max_dist, tol;
+    double disk_in, disk_out, disk_tscale;
+    int max_steps;
+    int method;  /* IntegrationMethod */
+    int has_disk;
+    int flags;   /* BHRT_FLAG_* */
+    int spin0;   /* blackhole->spin == 0.0 */
+} bhrt_scene_k;
+
+typedef struct {
+    /* pixel -> direction (calculate_ray_direction, raytracer.c:999-1039) */
+    double fwd[3], right[3], up[3];
+    double plane_w, plane_h;
+    int width, height;
+    bhrt_rows rows;
+    /* shared origin (integrate_photon_path set-up, raytracer.c:355-466) */
+    double pos[3];                   /* Cartesian origin                        */
+    double r0, th0, ph0;             /* cartesian_to_spherical(origin)          */
+    double st_cp, st_sp, ct, ct_cp, ct_sp, st, neg_sp, cp, r_st; /* trig products */
+    double g_tt, g_rr, g_hh;         /* calculate_schwarzschild_metric(r0)      */
+    double p0[3];                    /* spherical_to_cartesian(r0, th0, ph0)    */
+    int use_approx;                  /* r0 > 15 rs                              */
+    int st_tiny;                     /* fabs(sin th0) < BH_EPSILON              */
+} bhrt_camera_k;
+
+typedef struct {
+    bhrt_scene_k sc;
+    int src;              /* BHRT_SRC_*                                       */
+    int n;                /* rays in this launch                              */
+    int refill;           /* refill a wave once >= refill lanes are idle      */
+    const Ray* rays;      /* BHRT_SRC_RAYS: device AoS input                  */
+    double* init;         /* BHRT_SRC_RAYS: [BHRT_INIT_FIELDS][n] initial state */
+    bhrt_camera_k cam;    /* BHRT_SRC_CAMERA                                  */
+    bhrt_frame_soa out;   /* device SoA outputs; NULL fields skipped          */
+    unsigned long long* ctl; /* [0] queue head, [1..5] counters; zeroed per launch */
+} bhrt_kparams;
+
+/* launch helpers implemented in geodesic.hip; return 0 or a hipError_t value.
+ * bhrt_launch_trace records ev0/ev1 (hipEvent_t, may be NULL) around the trace kernel
+ * itself, not the set-up or colour passes. */
+int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0, void* ev1);
+int bhrt_launch_path(const bhrt_kparams* kp, const double* origin4, const double* dir3,
+                     Vector3D* d_path, int max_positions, int* d_num, int num_positions_in,
+                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

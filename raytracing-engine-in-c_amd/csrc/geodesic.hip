@@ -1,0 +1,746 @@
+// geodesic.hip -- MI355X (gfx950) kernels of the geodesic ray tracer.
+//
+// One lane = one ray, FP64 throughout, the integrated state in VGPRs. What each lane
+// computes is the reference's integrate_photon_path / trace_ray (src/raytracer.c:338-767,
+// with rk4_integrate / rkf45_integrate of src/math_util.c:162-457 inlined), reproduced with
+// its quirks: the index-shifted ray_derivatives (raytracer.c:44-154), the clamps, the
+// radius step schedule and the zero-acceleration "Kerr" branch. See DESIGN.md section 2.
+//
+// Restructurings that leave every pinned output unchanged:
+//   * trace_ray stores the whole path and scans it for the first disk crossing afterwards
+//     (raytracer.c:698-759); here each segment is tested as soon as it exists and the lane
+//     stops at the first hit.
+//   * RKF45 never adapts h (raytracer.c:556-571 recomputes it from r), so a rejected attempt
+//     leaves the state at a fixed point that rejects until max_steps; the lane jumps there.
+//   * derivatives[6..7] are never written by the reference (uninitialised malloc); they are 0
+//     here, so state[6..7] are per-ray constants.
+//
+// Divergence: rays live from 1 to max_steps iterations. The grid is persistent; every
+// wavefront keeps 64 rays in flight and, once `refill` of its lanes have finished, claims
+// that many new ray indices from a global queue with ONE atomic and initialises them in
+// the idle lanes (ballot + popcount + lane rank), so a long ray never holds 63 idle lanes.
+//
+// Arithmetic: FP contraction is off by default (BHRT_CONTRACT=0): the kernel then rounds
+// every +,-,* like the reference's x86-64 build, and the only differences left are the
+// last-ulp differences between OCML and glibc sin/cos/acos/atan2/pow.
+#include <hip/hip_runtime.h>
+
+#include "bhrt_kernel.h"
+
+#ifndef BHRT_CONTRACT
+#define BHRT_CONTRACT 0
+#endif
+#if BHRT_CONTRACT
+#pragma clang fp contract(fast)
+#else
+#pragma clang fp contract(off)
+#endif
+
+namespace {
+
+constexpr double kEps = 1.0e-10;  // BH_EPSILON (math_util.h:21)
+constexpr double kTwoPi = 6.28318530717958647692;
+
+using Scene = bhrt_scene_k;
+
+struct Counters {
+    unsigned rays = 0, iters = 0, full = 0, far_ = 0, kerr = 0;
+};
+
+// ray_derivatives (raytracer.c:44-154). y = (t, r, theta, phi, tdot, rdot) of the caller,
+// read -- as the reference does -- as (r, theta, phi, v_r, v_theta, v_phi).
+template <bool SPIN0>
+__device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const Scene& sc,
+                                    bool far_ok, Counters& n) {
+    d[0] = y[3];
+    d[1] = y[4];
+    d[2] = y[5];
+    if (far_ok && y[0] > sc.rs_x15) {  // weak-field branch, no NaN/clamp pass (:65-86)
+        d[3] = 0.0;
+        d[4] = 0.0;
+        d[5] = y[5] * (sc.two_m / (y[0] * y[0]));
+        n.far_++;
+        return;
+    }
+    if (SPIN0) {  // :92-130
+        double r = y[0];
+        double rsq = r * r;
+        double st, ct;
+        sincos(y[1], &st, &ct);
+        double st2 = st * st;
+        if (r <= sc.rs_x1_5) {
+            r = sc.rs_x1_5;
+            rsq = r * r;
+        }
+        if (fabs(st) < 0.01) {
+            st = (st >= 0.0) ? 0.01 : -0.01;
+            st2 = st * st;
+        }
+        const double f = 1.0 - sc.rs / r;
+        const double term1 = -sc.M / (rsq * f) * f;
+        const double term2 = r * y[4] * y[4];
+        const double term3 = r * st2 * y[5] * y[5];
+        d[3] = term1 + term2 + term3;
+        d[4] = -2.0 * y[3] * y[4] / r + st * ct * y[5] * y[5];
+        d[5] = -2.0 * y[3] * y[5] / r - 2.0 * y[4] * y[5] * ct / st;
+        n.full++;
+    } else {  // :131-138
+        d[3] = 0.0;
+        d[4] = 0.0;
+        d[5] = 0.0;
+        n.kerr++;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++)  // :141-145
+        if (!isfinite(d[i])) d[i] = 0.0;
+#pragma unroll
+    for (int i = 3; i < 6; i++)  // :148-153
+        if (fabs(d[i]) > 10.0) d[i] = (d[i] > 0.0) ? 10.0 : -10.0;
+}
+
+// rk4_integrate (math_util.c:162-207) on the six live components; the running sum
+// ((k1 + 2k2) + 2k3) + k4 is the reference's left-to-right evaluation order.
+template <bool SPIN0>
+__device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& sc, bool far_ok,
+                                         Counters& n) {
+    double k[6], acc[6], yt[6];
+    const double hh = 0.5 * h;
+    rhs<SPIN0>(y, k, sc, far_ok, n);
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        acc[i] = k[i];
+        yt[i] = y[i] + hh * k[i];
+    }
+    rhs<SPIN0>(yt, k, sc, far_ok, n);
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        acc[i] = acc[i] + 2.0 * k[i];
+        yt[i] = y[i] + hh * k[i];
+    }
+    rhs<SPIN0>(yt, k, sc, far_ok, n);
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        acc[i] = acc[i] + 2.0 * k[i];
+        yt[i] = y[i] + h * k[i];
+    }
+    rhs<SPIN0>(yt, k, sc, far_ok, n);
+#pragma unroll
+    for (int i = 0; i < 6; i++) y[i] += h * (acc[i] + k[i]) / 6.0;
+}
+
+// rkf45_integrate (math_util.c:212-457), n = 6. Returns true on accept (y <- y5).
+template <bool SPIN0>
+__device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Scene& sc,
+                                              bool far_ok, Counters& n) {
+    constexpr double b21 = 1.0 / 4.0;
+    constexpr double b31 = 3.0 / 32.0, b32 = 9.0 / 32.0;
+    constexpr double b41 = 1932.0 / 2197.0, b42 = -7200.0 / 2197.0, b43 = 7296.0 / 2197.0;
+    constexpr double b51 = 439.0 / 216.0, b52 = -8.0, b53 = 3680.0 / 513.0,
+                     b54 = -845.0 / 4104.0;
+    constexpr double b61 = -8.0 / 27.0, b62 = 2.0, b63 = -3544.0 / 2565.0,
+                     b64 = 1859.0 / 4104.0, b65 = -11.0 / 40.0;
+    constexpr double c1 = 25.0 / 216.0, c3 = 1408.0 / 2565.0, c4 = 2197.0 / 4104.0,
+                     c5 = -1.0 / 5.0;
+    constexpr double d1 = 16.0 / 135.0, d3 = 6656.0 / 12825.0, d4 = 28561.0 / 56430.0,
+                     d5 = -9.0 / 50.0, d6 = 2.0 / 55.0;
+    double k1[6], k2[6], k3[6], k4[6], k5[6], k6[6], yt[6];
+    rhs<SPIN0>(y, k1, sc, far_ok, n);
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 6; i++) bad |= !isfinite(k1[i]);  // :318-333
+    if (bad) return false;
+    const double hb21 = h * b21;
+#pragma unroll
+    for (int i = 0; i < 6; i++) yt[i] = y[i] + hb21 * k1[i];
+    rhs<SPIN0>(yt, k2, sc, far_ok, n);
+#pragma unroll
+    for (int i = 0; i < 6; i++) yt[i] = y[i] + h * (b31 * k1[i] + b32 * k2[i]);
+    rhs<SPIN0>(yt, k3, sc, far_ok, n);
+#pragma unroll
+    for (int i = 0; i < 6; i++) yt[i] = y[i] + h * (b41 * k1[i] + b42 * k2[i] + b43 * k3[i]);
+    rhs<SPIN0>(yt, k4, sc, far_ok, n);
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+        yt[i] = y[i] + h * (b51 * k1[i] + b52 * k2[i] + b53 * k3[i] + b54 * k4[i]);
+    rhs<SPIN0>(yt, k5, sc, far_ok, n);
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+        yt[i] = y[i] + h * (b61 * k1[i] + b62 * k2[i] + b63 * k3[i] + b64 * k4[i] + b65 * k5[i]);
+    rhs<SPIN0>(yt, k6, sc, far_ok, n);
+    double y5[6];
+    double max_error = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {  // :367-391
+        const double y4 = y[i] + h * (c1 * k1[i] + c3 * k3[i] + c4 * k4[i] + c5 * k5[i]);
+        y5[i] = y[i] + h * (d1 * k1[i] + d3 * k3[i] + d4 * k4[i] + d5 * k5[i] + d6 * k6[i]);
+        double scale = fmax(fabs(y[i]), fabs(y5[i]));
+        if (scale < kEps) scale = kEps;
+        max_error = fmax(max_error, fabs(y5[i] - y4) / scale);
+    }
+    if (max_error / sc.tol <= 1.0) {  // :402-434
+#pragma unroll
+        for (int i = 0; i < 6; i++) y[i] = y5[i];
+        return true;
+    }
+    return false;
+}
+
+// spherical_to_cartesian (spacetime.c:229-237)
+__device__ __forceinline__ void sph2cart(double r, double th, double ph, double& x, double& y,
+                                         double& z) {
+    double st, ct, sp, cp;
+    sincos(th, &st, &ct);
+    sincos(ph, &sp, &cp);
+    x = r * st * cp;
+    y = r * st * sp;
+    z = r * ct;
+}
+
+__device__ __forceinline__ double len3(double x, double y, double z) {
+    return sqrt((x * x + y * y) + z * z);  // vector3D_length (math_util.c:85-113)
+}
+
+struct Ray_ {
+    double y[6];        // (t, r, theta, phi, tdot, rdot)
+    double y6, y7;      // (thetadot, phidot): constants, see header
+    double dx, dy, dz;  // Ray.direction as given (disk test)
+    double px, py, pz;  // current Cartesian position
+    double qx, qy, qz;  // disk hit point
+    double dist;
+    int k;              // iterations executed
+    bool far_ok;        // use_analytic_approx && impact_parameter > 0
+};
+
+// Trig-free part of integrate_photon_path's set-up (raytracer.c:355-466): the initial
+// velocities, dt/dlambda from the null condition, E, L, b. s_* are products of the origin's
+// sin/cos, g_* the metric at the origin.
+__device__ __forceinline__ void init_velocity(Ray_& R, double nx, double ny, double nz,
+                                              double r, double st_cp, double st_sp, double ct,
+                                              double ct_cp, double ct_sp, double st,
+                                              double neg_sp, double cp, double r_st,
+                                              bool st_tiny, double g_tt, double g_rr,
+                                              double g_hh, bool use_approx) {
+    const double vr = st_cp * nx + st_sp * ny + ct * nz;            // :389-391
+    const double vth = (ct_cp * nx + ct_sp * ny - st * nz) / r;     // :394-396
+    double vph = (neg_sp * nx + cp * ny) / r_st;                    // :399
+    if (st_tiny) vph = 0.0;                                         // :402-405
+    double dt2 = -(g_rr * vr * vr + g_hh * vth * vth + g_hh * vph * vph) / g_tt;  // :416-418
+    if (dt2 < 0.0) dt2 = 0.0;
+    const double vt = sqrt(dt2);
+    const double b = fabs((g_hh * vph) / (-g_tt * vt));  // |L / E| (:437-448)
+    R.far_ok = use_approx && (b > 0.0);
+    R.y[4] = vt;
+    R.y[5] = vr;
+    R.y6 = isfinite(vth) ? vth : 0.0;  // recovery of :543-548 for the constant components
+    R.y7 = isfinite(vph) ? vph : 0.0;
+}
+
+__device__ __forceinline__ void normalize3(double x, double y, double z, double& nx, double& ny,
+                                           double& nz) {
+    const double l = len3(x, y, z);  // vector3D_normalize (math_util.c:115-122)
+    if (l < kEps) {
+        nx = ny = nz = 0.0;
+    } else {
+        const double inv = 1.0 / l;
+        nx = x * inv;
+        ny = y * inv;
+        nz = z * inv;
+    }
+}
+
+// Full per-ray set-up for an arbitrary origin (ray arrays, single-ray path kernel).
+__device__ __forceinline__ void ray_init_general(Ray_& R, double t0, double ox, double oy,
+                                                 double oz, double dx, double dy, double dz,
+                                                 const Scene& sc) {
+    R.dx = dx;
+    R.dy = dy;
+    R.dz = dz;
+    double nx, ny, nz;
+    normalize3(dx, dy, dz, nx, ny, nz);
+    const double r = sqrt(ox * ox + oy * oy + oz * oz);  // cartesian_to_spherical
+    const double th = (r > kEps) ? acos(oz / r) : 0.0;
+    double ph = atan2(oy, ox);
+    if (ph < 0.0) ph += kTwoPi;
+    double st, ct, sp, cp;
+    sincos(th, &st, &ct);
+    sincos(ph, &sp, &cp);
+    const double rm = (r <= sc.rs_eps) ? sc.rs_eps : r;  // calculate_schwarzschild_metric
+    const double g_tt = -(1.0 - sc.rs / rm);
+    const double g_rr = 1.0 / (1.0 - sc.rs / rm);
+    const double g_hh = rm * rm;  // g_thth = g_phph (sin^2(pi/2) == 1)
+    init_velocity(R, nx, ny, nz, r, st * cp, st * sp, ct, ct * cp, ct * sp, st, -sp, cp, r * st,
+                  fabs(st) < kEps, g_tt, g_rr, g_hh, r > sc.rs_x15);
+    R.y[0] = t0;
+    R.y[1] = r;
+    R.y[2] = th;
+    R.y[3] = ph;
+    R.px = r * st * cp;  // spherical_to_cartesian of the initial state (:498-501)
+    R.py = r * st * sp;
+    R.pz = r * ct;
+    R.dist = 0.0;
+    R.k = 0;
+}
+
+// calculate_ray_direction (raytracer.c:1013-1038) for pixel-centre ray i of the shard
+__device__ __forceinline__ void camera_dir(const bhrt_camera_k& cm, int i, double& dx,
+                                           double& dy, double& dz) {
+    const int W = cm.width;
+    const int j = i / W, px = i - j * W;
+    int py = j;
+    if (cm.rows.num_shards > 1) {
+        const int B = cm.rows.row_block;
+        py = ((j / B) * cm.rows.num_shards + cm.rows.shard) * B + j % B;
+    }
+    const double ndcx = (2.0 * ((px + 0.5) / W) - 1.0) * cm.plane_w;
+    const double ndcy = (1.0 - 2.0 * ((py + 0.5) / cm.height)) * cm.plane_h;
+    double vx = cm.fwd[0], vy = cm.fwd[1], vz = cm.fwd[2];
+    vx = vx + cm.right[0] * ndcx;
+    vy = vy + cm.right[1] * ndcx;
+    vz = vz + cm.right[2] * ndcx;
+    vx = vx + cm.up[0] * ndcy;
+    vy = vy + cm.up[1] * ndcy;
+    vz = vz + cm.up[2] * ndcy;
+    normalize3(vx, vy, vz, dx, dy, dz);
+}
+
+// Camera ray set-up: the origin is shared, so only the direction-dependent part runs here.
+__device__ __forceinline__ void ray_init_camera(Ray_& R, const bhrt_camera_k& cm, int i) {
+    camera_dir(cm, i, R.dx, R.dy, R.dz);
+    double nx, ny, nz;
+    normalize3(R.dx, R.dy, R.dz, nx, ny, nz);  // integrate_photon_path normalises again
+    init_velocity(R, nx, ny, nz, cm.r0, cm.st_cp, cm.st_sp, cm.ct, cm.ct_cp, cm.ct_sp, cm.st,
+                  cm.neg_sp, cm.cp, cm.r_st, cm.st_tiny != 0, cm.g_tt, cm.g_rr, cm.g_hh,
+                  cm.use_approx != 0);
+    R.y[0] = 0.0;
+    R.y[1] = cm.r0;
+    R.y[2] = cm.th0;
+    R.y[3] = cm.ph0;
+    R.px = cm.p0[0];
+    R.py = cm.p0[1];
+    R.pz = cm.p0[2];
+    R.dist = 0.0;
+    R.k = 0;
+}
+
+// check_disk_intersection (raytracer.c:159-196), plane "normal" = previous path point
+__device__ __forceinline__ bool disk_test(Ray_& R, double nx, double ny, double nz,
+                                          const Scene& sc) {
+    const double den = (R.dx * nx + R.dy * ny) + R.dz * nz;
+    if (fabs(den) < kEps) return false;
+    const double t = -((R.px * nx + R.py * ny) + R.pz * nz) / den;
+    if (t < 0.0) return false;
+    const double qx = R.px + R.dx * t, qy = R.py + R.dy * t, qz = R.pz + R.dz * t;
+    const double rxy = sqrt(qx * qx + qy * qy);
+    if (rxy >= sc.disk_in && rxy <= sc.disk_out) {
+        R.qx = qx;
+        R.qy = qy;
+        R.qz = qz;
+        return true;
+    }
+    return false;
+}
+
+enum Term : int { T_NONE = 0, T_HORIZON, T_DISK, T_MAXDIST, T_MAXSTEPS };
+
+// One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
+// on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
+template <int METHOD, bool DISK, bool SPIN0>
+__device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n) {
+#pragma unroll
+    for (int i = 0; i < 6; i++)  // :543-548
+        if (!isfinite(R.y[i])) R.y[i] = (i < 4) ? 1.0 : 0.0;
+    // step schedule (:556-571), written as selects so the first true test wins
+    const double r = R.y[1];
+    double h = sc.h_far;
+    h = (r < sc.rs_x15) ? sc.h_15 : h;
+    h = (r < sc.rs_x5) ? sc.h_5 : h;
+    h = (r < sc.rs_x2_5) ? sc.h_2_5 : h;
+    h = fmin(h, 0.1);
+    bool moved = true;
+    n.iters++;
+    if (METHOD == INTEGRATOR_RK4) {
+        rk4_step<SPIN0>(R.y, h, sc, R.far_ok, n);
+    } else if (METHOD == INTEGRATOR_RKF45) {
+        moved = rkf45_attempt<SPIN0>(R.y, h, sc, R.far_ok, n);
+    } else {
+        moved = false;  // LEAPFROG / YOSHIDA: "not implemented", state unchanged (:616-624)
+    }
+    double x, y, z;
+    sph2cart(R.y[1], R.y[2], R.y[3], x, y, z);
+    const double ox = R.px, oy = R.py, oz = R.pz;
+    R.dist += len3(x - ox, y - oy, z - oz);
+    R.px = x;
+    R.py = y;
+    R.pz = z;
+    R.k++;
+    // segment k = (p_k, p_{k-1}) is stored and scanned by trace_ray iff k < max_steps
+    if (DISK && R.k < sc.max_steps && disk_test(R, ox, oy, oz, sc)) {
+        R.dist += len3(R.qx - ox, R.qy - oy, R.qz - oz);
+        return T_DISK;
+    }
+    if (R.y[1] <= sc.rs_x1_05) return T_HORIZON;
+    if (R.dist >= sc.max_dist) return T_MAXDIST;
+    if (!moved) {
+        // Fixed point: every later iteration repeats this one with p_j = p_{j-1} = p_k.
+        // Only the duplicate segment (p_k, p_k) is new, and only if p_k != p_{k-1}.
+        if (DISK && R.k + 1 < sc.max_steps && (x != ox || y != oy || z != oz) &&
+            disk_test(R, x, y, z, sc)) {
+            R.k++;
+            R.dist += len3(R.qx - x, R.qy - y, R.qz - z);
+            return T_DISK;
+        }
+        R.k = sc.max_steps;
+        return T_MAXSTEPS;
+    }
+    if (R.k >= sc.max_steps) return T_MAXSTEPS;
+    return T_NONE;
+}
+
+// fill_hit_info (raytracer.c:299-333) / the disk branch of trace_ray (:728-753)
+__device__ __forceinline__ void store_hit(const bhrt_frame_soa& s, int i, const Ray_& R,
+                                          int term, const Scene& sc) {
+    int result, steps;
+    double hx, hy, hz, tdil, sx = 0.0, sy = 0.0, sz = 0.0;
+    if (term == T_DISK) {
+        result = RAY_DISK;
+        steps = R.k;
+        hx = R.qx;
+        hy = R.qy;
+        hz = R.qz;
+        tdil = 1.0 / sqrt(1.0 - sc.rs / len3(R.qx, R.qy, R.qz));
+    } else {
+        result = term == T_HORIZON ? RAY_HORIZON
+                                   : (term == T_MAXDIST ? RAY_MAX_DISTANCE : RAY_MAX_STEPS);
+        steps = term == T_MAXSTEPS ? R.k : R.k - 1;
+        hx = R.px;
+        hy = R.py;
+        hz = R.pz;
+        tdil = 1.0 / sqrt(1.0 - sc.rs / R.y[1]);
+        if (term == T_MAXDIST) normalize3(R.y[5], R.y6, R.y7, sx, sy, sz);  // state[5..7]
+    }
+    if (s.result) s.result[i] = result;
+    if (s.steps) s.steps[i] = steps;
+    if (s.hit_x) s.hit_x[i] = hx;
+    if (s.hit_y) s.hit_y[i] = hy;
+    if (s.hit_z) s.hit_z[i] = hz;
+    if (s.distance) s.distance[i] = R.dist;
+    if (s.time_dilation) s.time_dilation[i] = tdil;
+    if (s.sky_x) s.sky_x[i] = sx;
+    if (s.sky_y) s.sky_y[i] = sy;
+    if (s.sky_z) s.sky_z[i] = sz;
+}
+
+__device__ __forceinline__ void load_init(const bhrt_kparams& kp, int i, Ray_& R) {
+    const double* f = kp.init;
+    const long n = kp.n;
+#pragma unroll
+    for (int j = 0; j < 6; j++) R.y[j] = f[j * n + i];
+    R.y6 = f[6 * n + i];
+    R.y7 = f[7 * n + i];
+    R.dx = f[8 * n + i];
+    R.dy = f[9 * n + i];
+    R.dz = f[10 * n + i];
+    R.px = f[11 * n + i];
+    R.py = f[12 * n + i];
+    R.pz = f[13 * n + i];
+    R.far_ok = f[14 * n + i] != 0.0;
+    R.dist = 0.0;
+    R.k = 0;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
+    unsigned long long s = v;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    return s;
+}
+
+// Set-up of an array of rays with arbitrary origins: [BHRT_INIT_FIELDS][n] state table.
+__global__ __launch_bounds__(256) void k_init_rays(const bhrt_kparams kp) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += gridDim.x * blockDim.x) {
+        const Ray ray = kp.rays[i];
+        Ray_ R;
+        ray_init_general(R, 0.0, ray.origin.x, ray.origin.y, ray.origin.z, ray.direction.x,
+                         ray.direction.y, ray.direction.z, kp.sc);
+        double* f = kp.init;
+        const long n = kp.n;
+#pragma unroll
+        for (int j = 0; j < 6; j++) f[j * n + i] = R.y[j];
+        f[6 * n + i] = R.y6;
+        f[7 * n + i] = R.y7;
+        f[8 * n + i] = R.dx;
+        f[9 * n + i] = R.dy;
+        f[10 * n + i] = R.dz;
+        f[11 * n + i] = R.px;
+        f[12 * n + i] = R.py;
+        f[13 * n + i] = R.pz;
+        f[14 * n + i] = R.far_ok ? 1.0 : 0.0;
+    }
+}
+
+// Persistent trace kernel: grid = what is resident; each wave refills idle lanes from the
+// global queue kp.ctl[0] (one returning atomic per refill).
+template <int METHOD, bool DISK, int SRC, bool SPIN0>
+__global__ __launch_bounds__(256) void k_trace(const bhrt_kparams kp) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    Counters n;
+    Ray_ R;
+    int rid = 0;
+    bool live = false;
+    bool exhausted = false;  // wave-uniform
+    for (;;) {
+        const unsigned long long live_mask = __ballot(live);
+        int n_live = __popcll(live_mask);
+        if (!exhausted && (64 - n_live >= kp.refill || n_live == 0)) {
+            const int need = 64 - n_live;
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(kp.ctl, (unsigned long long)need);
+            base = __shfl(base, 0);
+            exhausted = base + (unsigned long long)need >= (unsigned long long)kp.n;
+            if (!live) {
+                const unsigned long long id = base + __popcll(~live_mask & below);
+                if (id < (unsigned long long)kp.n) {
+                    rid = (int)id;
+                    if (SRC == BHRT_SRC_CAMERA) ray_init_camera(R, kp.cam, rid);
+                    else load_init(kp, rid, R);
+                    n.rays++;
+                    live = true;
+                    if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
+                        store_hit(kp.out, rid, R, T_MAXSTEPS, kp.sc);
+                        live = false;
+                    }
+                }
+            }
+            n_live = __popcll(__ballot(live));
+        }
+        if (n_live == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        if (live) {
+            const int term = ray_iterate<METHOD, DISK, SPIN0>(R, kp.sc, n);
+            if (term != T_NONE) {
+                store_hit(kp.out, rid, R, term, kp.sc);
+                live = false;
+            }
+        }
+    }
+    const unsigned long long s0 = wave_sum(n.rays), s1 = wave_sum(n.iters),
+                             s2 = wave_sum(n.full), s3 = wave_sum(n.far_),
+                             s4 = wave_sum(n.kerr);
+    if (lane == 0) {
+        if (s0) atomicAdd(kp.ctl + 1, s0);
+        if (s1) atomicAdd(kp.ctl + 2, s1);
+        if (s2) atomicAdd(kp.ctl + 3, s2);
+        if (s3) atomicAdd(kp.ctl + 4, s3);
+        if (s4) atomicAdd(kp.ctl + 5, s4);
+    }
+}
+
+__device__ __forceinline__ double clampd(double v, double lo, double hi) {
+    if (v < lo) return lo;  // math_util.c:505-509 (NaN passes through)
+    if (v > hi) return hi;
+    return v;
+}
+
+// Frame colour contract, one elementwise pass after the trace:
+// calculate_disk_temperature + temperature_to_rgb (+ apply_relativistic_effects) for disk
+// hits, black for the horizon, the sky gradient of raytracer.c:1150-1157 otherwise.
+template <int SRC>
+__global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
+    const Scene& sc = kp.sc;
+    const bhrt_frame_soa& s = kp.out;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += gridDim.x * blockDim.x) {
+        double dx, dy, dz;
+        if (SRC == BHRT_SRC_CAMERA) {
+            camera_dir(kp.cam, i, dx, dy, dz);
+        } else {
+            dx = kp.rays[i].direction.x;
+            dy = kp.rays[i].direction.y;
+            dz = kp.rays[i].direction.z;
+        }
+        const int res = s.result[i];
+        double r, g, b;
+        if (res == RAY_DISK) {
+            const double hx = s.hit_x[i], hy = s.hit_y[i];
+            const double rxy = sqrt(hx * hx + hy * hy);  // raytracer.c:201-228
+            double nr = (rxy - sc.disk_in) / (sc.disk_out - sc.disk_in);
+            nr = clampd(nr, 0.0, 1.0);
+            const double T = clampd(sc.disk_tscale * (2000.0 + 18000.0 * pow(1.0 - nr, 0.75)),
+                                    1000.0, 40000.0);  // math_util.c:463-503
+            const double t = (T - 1000.0) / (40000.0 - 1000.0);
+            r = (t < 0.5) ? t * 2.0 : 1.0;
+            g = (t < 0.25) ? 0.0 : ((t < 0.75) ? (t - 0.25) * 2.0 : 1.0);
+            b = (t < 0.5) ? 0.0 : (t - 0.5) * 2.0;
+            const double br = 0.2 + 0.8 * (t * t);
+            r *= br;
+            g *= br;
+            b *= br;
+            if (sc.flags & BHRT_FLAG_DOPPLER) {  // raytracer.c:233-294
+                double sp, cp;
+                sincos(atan2(hy, hx), &sp, &cp);
+                const double dop = 1.0 + ((dx * -sp + dy * cp) + dz * 0.0) * 0.5;
+                const double z = dop / (1.0 / sqrt(1.0 - sc.rs / rxy));
+                if (z < 1.0) {
+                    b *= z;
+                    r = fmin(1.0, r * (2.0 - z));
+                } else {
+                    r *= 2.0 - z;
+                    b = fmin(1.0, b * z);
+                }
+                const double beam = pow(dop, 4.0);
+                r = clampd(r * beam, 0.0, 1.0);
+                g = clampd(g * beam, 0.0, 1.0);
+                b = clampd(b * beam, 0.0, 1.0);
+            }
+        } else if (res == RAY_HORIZON) {
+            r = g = b = 0.0;
+        } else {
+            const double t = 0.5 * (dy + 1.0);
+            r = (1.0 - t) * 1.0 + t * 0.5;
+            g = (1.0 - t) * 1.0 + t * 0.7;
+            b = (1.0 - t) * 1.0 + t * 1.0;
+        }
+        s.rgb_r[i] = r;
+        s.rgb_g[i] = g;
+        s.rgb_b[i] = b;
+    }
+}
+
+// integrate_photon_path with a recorded path (one ray, one lane). The output hit goes to
+// element 0 of kp.out; the path and the stored-point count to path / d_num.
+template <int METHOD, bool SPIN0>
+__global__ void k_path(const bhrt_kparams kp, double t0, double ox, double oy, double oz,
+                       double dx, double dy, double dz, Vector3D* path, int max_positions,
+                       int* d_num, int num_in) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    Counters n;
+    Ray_ R;
+    ray_init_general(R, t0, ox, oy, oz, dx, dy, dz, kp.sc);
+    int num = num_in;
+    if (path && max_positions > 0) {  // :504-507
+        path[0].x = R.px;
+        path[0].y = R.py;
+        path[0].z = R.pz;
+        num = 1;
+    }
+    int term = T_MAXSTEPS;
+    if (kp.sc.max_steps > 0) {
+        for (;;) {
+            const int k_before = R.k;
+            term = ray_iterate<METHOD, false, SPIN0>(R, kp.sc, n);
+            // positions of the iterations executed (a fixed-point jump repeats p_k)
+            for (int j = k_before; j < R.k && path && num >= 0 && num < max_positions; j++) {
+                path[num].x = R.px;
+                path[num].y = R.py;
+                path[num].z = R.pz;
+                num++;
+            }
+            if (term != T_NONE) break;
+        }
+    }
+    if (d_num) *d_num = num;
+    store_hit(kp.out, 0, R, term, kp.sc);
+}
+
+int g_cus = 0;
+
+int grid_for(const void* fn, int n) {
+    if (g_cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_cus <= 0) g_cus = 256;
+    }
+    int per_cu = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
+    if (per_cu <= 0) per_cu = 1;
+    long blocks = ((long)n + 255) / 256;
+    const long cap = (long)g_cus * per_cu;
+    if (blocks > cap) blocks = cap;
+    return blocks < 1 ? 1 : (int)blocks;
+}
+
+template <int METHOD, bool DISK, int SRC, bool SPIN0>
+int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    static int grid_cap = 0;  // resident workgroups for this instantiation
+    if (grid_cap == 0)
+        grid_cap = grid_for(reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SRC, SPIN0>),
+                            1 << 30);
+    if (SRC == BHRT_SRC_RAYS) {
+        const int g = grid_for(reinterpret_cast<const void*>(&k_init_rays), kp.n);
+        k_init_rays<<<g, 256, 0, st>>>(kp);
+    }
+    int blocks = (kp.n + 255) / 256;
+    if (blocks > grid_cap) blocks = grid_cap;
+    if (blocks < 1) blocks = 1;
+    if (ev0) (void)hipEventRecord(ev0, st);
+    k_trace<METHOD, DISK, SRC, SPIN0><<<blocks, 256, 0, st>>>(kp);
+    if (ev1) (void)hipEventRecord(ev1, st);
+    if (kp.out.rgb_r) {
+        const int g = grid_for(reinterpret_cast<const void*>(&k_colour<SRC>), kp.n);
+        k_colour<SRC><<<g, 256, 0, st>>>(kp);
+    }
+    return (int)hipGetLastError();
+}
+
+template <int METHOD, bool DISK, int SRC>
+int dispatch_spin(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+    return kp.sc.spin0 ? launch_t<METHOD, DISK, SRC, true>(kp, st, e0, e1)
+                       : launch_t<METHOD, DISK, SRC, false>(kp, st, e0, e1);
+}
+
+template <int METHOD, bool DISK>
+int dispatch_src(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+    return kp.src == BHRT_SRC_CAMERA
+               ? dispatch_spin<METHOD, DISK, BHRT_SRC_CAMERA>(kp, st, e0, e1)
+               : dispatch_spin<METHOD, DISK, BHRT_SRC_RAYS>(kp, st, e0, e1);
+}
+
+template <int METHOD>
+int dispatch_disk(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+    return kp.sc.has_disk ? dispatch_src<METHOD, true>(kp, st, e0, e1)
+                          : dispatch_src<METHOD, false>(kp, st, e0, e1);
+}
+
+template <int METHOD>
+void launch_path(const bhrt_kparams& kp, const double* o4, const double* d3, Vector3D* d_path,
+                 int max_positions, int* d_num, int num_in, hipStream_t st) {
+    if (kp.sc.spin0)
+        k_path<METHOD, true><<<1, 64, 0, st>>>(kp, o4[0], o4[1], o4[2], o4[3], d3[0], d3[1], d3[2],
+                                               d_path, max_positions, d_num, num_in);
+    else
+        k_path<METHOD, false><<<1, 64, 0, st>>>(kp, o4[0], o4[1], o4[2], o4[3], d3[0], d3[1],
+                                                d3[2], d_path, max_positions, d_num, num_in);
+}
+
+}  // namespace
+
+extern "C" int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0, void* ev1) {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipEvent_t e0 = static_cast<hipEvent_t>(ev0), e1 = static_cast<hipEvent_t>(ev1);
+    switch (kp->sc.method) {
+    case INTEGRATOR_RK4: return dispatch_disk<INTEGRATOR_RK4>(*kp, st, e0, e1);
+    case INTEGRATOR_RKF45: return dispatch_disk<INTEGRATOR_RKF45>(*kp, st, e0, e1);
+    default: return dispatch_disk<INTEGRATOR_LEAPFROG>(*kp, st, e0, e1);  // no-op integrators
+    }
+}
+
+extern "C" int bhrt_launch_path(const bhrt_kparams* kp, const double* o4, const double* d3,
+                                Vector3D* d_path, int max_positions, int* d_num, int num_in,
+                                void* stream) {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    switch (kp->sc.method) {
+    case INTEGRATOR_RK4:
+        launch_path<INTEGRATOR_RK4>(*kp, o4, d3, d_path, max_positions, d_num, num_in, st);
+        break;
+    case INTEGRATOR_RKF45:
+        launch_path<INTEGRATOR_RKF45>(*kp, o4, d3, d_path, max_positions, d_num, num_in, st);
+        break;
+    default:
+        launch_path<INTEGRATOR_LEAPFROG>(*kp, o4, d3, d_path, max_positions, d_num, num_in, st);
+        break;
+    }
+    return (int)hipGetLastError();
+}

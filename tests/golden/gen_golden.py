@@ -1,0 +1,324 @@
+"""Generate tests/golden/*.npz from the COMPILED REFERENCE (oracle/_ref/libref.so).
+
+Run in the build container only (the reference sources are not on the GPU box):
+
+    make -C oracle ref && python tests/golden/gen_golden.py
+
+libref.so is built by oracle/Makefile from the unmodified sources under /root/reference/src.
+Every output below is produced by reference code: trace_ray / integrate_photon_path /
+bh_trace_rays_batch / trace_pixel / the shading functions, driven by oracle/ref_driver.c
+(which adds only the pixel->direction restatement of the static calculate_ray_direction and
+the RKF45 + disk composition of SURVEY.md 8(d) C3). The reference's debug printing goes to
+/dev/null while it runs.
+
+Fixture contents are data only: inputs (scene, camera, rays) and the reference's outputs.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+from bhrt import abi, configs  # noqa: E402
+import oracle as orc  # noqa: E402
+
+REF = orc.reference()
+L = REF.lib
+P = C.POINTER
+
+
+def scene_arrays(bh, dk, cfg):
+    d = {"bh": np.array([getattr(bh, f) for f, _ in abi.BlackHoleParams._fields_]),
+         "cfg_f": np.array([cfg.time_step, cfg.max_ray_distance, cfg.tolerance]),
+         "cfg_steps": np.array(cfg.max_integration_steps, dtype=np.int64),
+         "has_disk": np.array(dk is not None)}
+    d["disk"] = (np.array([getattr(dk, f) for f, _ in abi.AccretionDiskParams._fields_])
+                 if dk is not None else np.zeros(6))
+    return d
+
+
+def ref_black_hole(mass, spin):
+    bh = abi.BlackHoleParams()
+    L.initialize_black_hole_params.argtypes = [P(abi.BlackHoleParams), C.c_double, C.c_double,
+                                               C.c_double]
+    L.initialize_black_hole_params(C.byref(bh), mass, spin, 0.0)
+    return bh
+
+
+def cam_array(cam):
+    return np.array([cam.position.x, cam.position.y, cam.position.z, cam.direction.x,
+                     cam.direction.y, cam.direction.z, cam.up.x, cam.up.y, cam.up.z, cam.fov_deg])
+
+
+def save(name, **arrays):
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
+    print("wrote", name, {k: v.shape for k, v in arrays.items() if hasattr(v, "shape")},
+          file=sys.stderr)
+
+
+def frames():
+    cases = [  # (fixture, config, camera, W, H)
+        ("frame_C1_B", "C1", "B", 32, 32),
+        ("frame_C1_A", "C1", "A", 24, 24),
+        ("frame_C2_B", "C2", "B", 48, 27),
+        ("frame_C2_A", "C2", "A", 32, 18),
+        ("frame_C2_V", "C2", "V", 32, 18),
+        ("frame_C3_B", "C3", "B", 32, 18),
+        ("frame_C4_B", "C4", "B", 64, 36),
+        ("frame_C5_B", "C5", "B", 48, 27),
+    ]
+    for name, cname, camname, W, H in cases:
+        c = configs.CONFIGS[cname]
+        bh = ref_black_hole(1.0, c.spin)
+        dk = abi.disk(bh.isco_radius, 20.0, 1.0, 1.0) if c.disk else None
+        cfg = abi.sim_config(0.1, 100.0, c.max_steps, c.tol)
+        cam = configs.camera(camname)
+        out = REF.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+        save(name, W=np.array(W), H=np.array(H), method=np.array(c.method),
+             flags=np.array(c.flags), cam=cam_array(cam), **scene_arrays(bh, dk, cfg),
+             **{"out_" + k: v for k, v in out.items()})
+    # Kerr a=0.99 with the disk down to its ISCO: r_xy < 2 gives NaN disk colour
+    bh = ref_black_hole(1.0, 0.99)
+    dk = abi.disk(bh.isco_radius, 20.0, 1.0, 1.0)
+    cfg = abi.sim_config(0.1, 100.0, 1000, 1e-6)
+    cam = configs.camera("A")
+    out = REF.render_frame(bh, dk, cfg, cam, 40, 40, abi.INTEGRATOR_RK4, abi.BHRT_FLAG_DOPPLER)
+    save("frame_kerr099_nan_A", W=np.array(40), H=np.array(40), method=np.array(0),
+         flags=np.array(abi.BHRT_FLAG_DOPPLER), cam=cam_array(cam), **scene_arrays(bh, dk, cfg),
+         **{"out_" + k: v for k, v in out.items()})
+
+
+def edge_rays():
+    rng = np.random.default_rng(20250523)
+    special = [
+        ((0, 0, 30), (0, 0, -1)), ((0, 0, 30), (0.2, 0, -1)), ((0, 0, 30), (0.5, 0, -1)),
+        ((0, 0, 30), (0.3, 0, -1)), ((30, 0, 0), (-1, 0, 0.1)),          # main.c:70-107
+        ((0, 0, 1.5), (1, 0, 0)), ((2.05, 0.1, 0), (0, 1, 0)),           # inside 1.05 rs
+        ((0.5, 0, 0), (0, 0, 1)), ((0, 0, 0), (1, 0, 0)),                # r = 0.5, r = 0
+        ((0, 0, 30), (0, 0, 0)), ((0, 0, 30), (0, 0, 1)),                # zero dir, outward
+        ((0, 0, -30), (0, 0, 1)), ((10, 0, 0), (0, 1, 0)),               # south pole, tangent
+        ((0, 0, 12), (1e-12, 0, -1)), ((7, 7, 0.001), (-1, -1, 0)),      # near-axis, in-plane
+        ((1e6, 0, 0), (-1, 0, 0)), ((-40, 25, 3), (1, -0.6, -0.1)),      # huge origin, far
+        ((75, 0, 0), (-1, 0.05, 0.02)), ((0, 80, 5), (0, -1, -0.05)),    # far-field branch
+        ((3.5, 0, 0.2), (0, 0.3, 1)), ((5.9, 0, 0), (0, 0, 1)),
+    ]
+    rays = [s for s in special]
+    for _ in range(160):
+        r = rng.uniform(2.5, 60.0)
+        u = rng.normal(size=3)
+        o = r * u / np.linalg.norm(u)
+        d = rng.normal(size=3)
+        rays.append((tuple(o), tuple(d)))
+    arr = np.zeros(len(rays), dtype=abi.RAY_DTYPE)
+    for i, (o, d) in enumerate(rays):
+        arr[i]["origin"] = o
+        arr[i]["direction"] = d
+    cases = [  # (name, spin, disk?, method, max_steps, tol, max_dist, flags)
+        ("rays_rk4_disk", 0.0, True, abi.INTEGRATOR_RK4, 1000, 1e-6, 100.0, 0),
+        ("rays_rk4_nodisk", 0.0, False, abi.INTEGRATOR_RK4, 1000, 1e-6, 100.0, 0),
+        ("rays_rk4_kerr_disk", 0.9, True, abi.INTEGRATOR_RK4, 1000, 1e-6, 100.0,
+         abi.BHRT_FLAG_DOPPLER),
+        ("rays_rkf45_nodisk", 0.0, False, abi.INTEGRATOR_RKF45, 400, 1e-6, 100.0, 0),
+        ("rays_rkf45_disk", 0.0, True, abi.INTEGRATOR_RKF45, 400, 1e-6, 100.0, 0),
+        ("rays_rkf45_kerr", 0.99, False, abi.INTEGRATOR_RKF45, 2000, 1e-8, 100.0, 0),
+        ("rays_leapfrog_disk", 0.0, True, abi.INTEGRATOR_LEAPFROG, 50, 1e-6, 100.0, 0),
+        ("rays_rk4_steps1", 0.0, True, abi.INTEGRATOR_RK4, 1, 1e-6, 100.0, 0),
+        ("rays_rk4_steps2", 0.0, True, abi.INTEGRATOR_RK4, 2, 1e-6, 100.0, 0),
+        ("rays_rk4_steps0", 0.0, True, abi.INTEGRATOR_RK4, 0, 1e-6, 100.0, 0),
+        ("rays_rk4_shortdist", 0.0, True, abi.INTEGRATOR_RK4, 1000, 1e-6, 0.5, 0),
+        ("rays_rk4_dt1", 0.0, True, abi.INTEGRATOR_RK4, 300, 1e-6, 100.0, 0),
+    ]
+    for name, spin, has_disk, method, steps, tol, mdist, flags in cases:
+        bh = ref_black_hole(1.0, spin)
+        dk = abi.disk(bh.isco_radius, 20.0, 1.0, 1.0) if has_disk else None
+        cfg = abi.sim_config(1.0 if name.endswith("dt1") else 0.1, mdist, steps, tol)
+        out = REF.trace_rays(arr, bh, dk, cfg, method, flags)
+        save(name, rays=arr.view(np.float64).reshape(-1, 6), method=np.array(method),
+             flags=np.array(flags), **scene_arrays(bh, dk, cfg),
+             **{"out_" + k: v for k, v in out.items()})
+
+
+def kat_main():
+    """main.c:190-226 + test_ray_tracing (main.c:61-126), through the bh_* context API."""
+    L.bh_initialize.restype = C.c_void_p
+    L.bh_configure_black_hole.argtypes = [C.c_void_p, C.c_double, C.c_double, C.c_double]
+    L.bh_configure_accretion_disk.argtypes = [C.c_void_p] + [C.c_double] * 4
+    L.bh_configure_simulation.argtypes = [C.c_void_p, C.c_double, C.c_double, C.c_int,
+                                          C.c_double]
+    L.bh_trace_rays_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    L.bh_shutdown.argtypes = [C.c_void_p]
+    ctx = L.bh_initialize()
+    assert L.bh_configure_black_hole(ctx, 1.0, 0.0, 0.0) == 0
+    assert L.bh_configure_accretion_disk(ctx, 6.0, 20.0, 1.0, 1.0) == 0
+    assert L.bh_configure_simulation(ctx, 0.1, 100.0, 1000, 1.0e-6) == 0
+    rays = np.zeros(5, dtype=abi.RAY_DTYPE)
+    rays["origin"] = [(0, 0, 30), (0, 0, 30), (0, 0, 30), (0, 0, 30), (30, 0, 0)]
+    rays["direction"] = [(0, 0, -1), (0.2, 0, -1), (0.5, 0, -1), (0.3, 0, -1), (-1, 0, 0.1)]
+    hits = np.zeros(5, dtype=abi.HIT_DTYPE)
+    REF.quiet(1)
+    rc = L.bh_trace_rays_batch(ctx, rays.ctypes.data, hits.ctypes.data, 5)
+    REF.quiet(0)
+    L.bh_shutdown(ctx)
+    assert rc == 0
+    save("kat_main5", rays=rays.view(np.float64).reshape(-1, 6), result=hits["result"],
+         steps=hits["steps"], hit_position=hits["hit_position"], distance=hits["distance"],
+         time_dilation=hits["time_dilation"])
+
+
+def shading():
+    """Scalar reference functions on the ray path (spacetime.c, raytracer.c:159-294,852,
+    math_util.c:463-503)."""
+    rng = np.random.default_rng(7)
+    d = {}
+    L.temperature_to_rgb.argtypes = [C.c_double, P(C.c_double * 3)]
+    temps = np.concatenate([[0.0, 999.0, 1000.0, 5000.0, 10750.0, 20500.0, 30250.0, 40000.0,
+                             45000.0, float("nan")], rng.uniform(500, 42000, 40)])
+    rgb = np.zeros((len(temps), 3))
+    for i, t in enumerate(temps):
+        o = (C.c_double * 3)()
+        L.temperature_to_rgb(t, C.byref(o))
+        rgb[i] = list(o)
+    d["t2rgb_in"], d["t2rgb_out"] = temps, rgb
+
+    L.calculate_disk_temperature.argtypes = [P(abi.Vector3D), P(abi.BlackHoleParams),
+                                             P(abi.AccretionDiskParams), P(C.c_double),
+                                             P(C.c_double * 3)]
+    L.apply_relativistic_effects.argtypes = [P(abi.Vector3D), P(abi.Vector3D),
+                                             P(abi.BlackHoleParams), P(C.c_double * 3),
+                                             P(C.c_double)]
+    bh = ref_black_hole(1.0, 0.0)
+    dk = abi.disk(6.0, 20.0, 1.0, 1.0)
+    pos = np.concatenate([[[10, 0, 0], [6, 0, 0], [20, 0, 0], [1.5, 0.5, 0], [0, 25, 1]],
+                          rng.uniform(-22, 22, (40, 3))])
+    vel = np.concatenate([[[0, 1, 0], [0, 0, -1], [1, 0, 0], [0, -1, 0], [0.3, 0.3, 0.9]],
+                          rng.normal(size=(40, 3))])
+    dt_out = np.zeros((len(pos), 4))
+    rel_out = np.zeros((len(pos), 4))
+    for i, (p, v) in enumerate(zip(pos, vel)):
+        T = C.c_double()
+        col = (C.c_double * 3)()
+        L.calculate_disk_temperature(C.byref(abi.v3(*p)), C.byref(bh), C.byref(dk), C.byref(T),
+                                     C.byref(col))
+        dt_out[i] = [T.value] + list(col)
+        dop = C.c_double()
+        L.apply_relativistic_effects(C.byref(abi.v3(*p)), C.byref(abi.v3(*v)), C.byref(bh),
+                                     C.byref(col), C.byref(dop))
+        rel_out[i] = list(col) + [dop.value]
+    d["disk_pos"], d["disk_vel"], d["disk_temp_out"], d["relativistic_out"] = pos, vel, dt_out, rel_out
+
+    L.halton_sequence.restype = C.c_double
+    L.halton_sequence.argtypes = [C.c_int, C.c_int]
+    hal = np.array([[i, b, L.halton_sequence(i, b)] for b in (2, 3, 5) for i in range(0, 40)])
+    d["halton"] = hal
+
+    spins = np.array([0.0, 0.1, 0.5, 0.9, 0.99, 0.998, 1.0])
+    d["bh_spins"] = spins
+    d["bh_params"] = np.array([[getattr(ref_black_hole(1.0, s), f)
+                                for f, _ in abi.BlackHoleParams._fields_] for s in spins])
+
+    L.check_disk_intersection.argtypes = [P(abi.Vector3D)] * 3 + [P(abi.AccretionDiskParams),
+                                                                  P(abi.Vector3D)]
+    cdi_in = rng.uniform(-20, 20, (300, 9))
+    cdi_in[:5, 6:] = 0.0  # zero "normal": parallel reject
+    cdi_out = np.zeros((300, 4))
+    for i, row in enumerate(cdi_in):
+        q = abi.Vector3D(0, 0, 0)
+        h = L.check_disk_intersection(C.byref(abi.v3(*row[0:3])), C.byref(abi.v3(*row[3:6])),
+                                      C.byref(abi.v3(*row[6:9])), C.byref(dk), C.byref(q))
+        cdi_out[i] = [h, q.x, q.y, q.z] if h else [0, 0, 0, 0]
+    d["cdi_in"], d["cdi_out"] = cdi_in, cdi_out
+
+    L.cartesian_to_spherical.argtypes = [P(abi.Vector3D), P(abi.Vector3D)]
+    L.spherical_to_cartesian.argtypes = [P(abi.Vector3D), P(abi.Vector3D)]
+    cs_in = np.concatenate([[[0, 0, 0], [0, 0, 5], [1, -1, 0], [-3, -4, 12]],
+                            rng.uniform(-50, 50, (40, 3))])
+    c2s = np.zeros_like(cs_in)
+    s2c = np.zeros_like(cs_in)
+    for i, p in enumerate(cs_in):
+        o = abi.Vector3D()
+        L.cartesian_to_spherical(C.byref(abi.v3(*p)), C.byref(o))
+        c2s[i] = [o.x, o.y, o.z]
+        L.spherical_to_cartesian(C.byref(o), C.byref(o2 := abi.Vector3D()))
+        s2c[i] = [o2.x, o2.y, o2.z]
+    d["cs_in"], d["c2s_out"], d["s2c_out"] = cs_in, c2s, s2c
+    save("shading", **d)
+
+
+def pixels():
+    """trace_pixel (raytracer.c:1044-1167) with ss_params = NULL: pins the result class and,
+    for non-disk pixels, the sky gradient of the pixel-centre direction. (For disk pixels the
+    reference returns an uninitialised colour, which is not recorded.)"""
+    L.trace_pixel.argtypes = [C.c_int] * 4 + [P(abi.Vector3D)] * 3 + [
+        C.c_double, P(abi.BlackHoleParams), P(abi.AccretionDiskParams), P(abi.SimulationConfig),
+        C.c_void_p, C.c_void_p, P(C.c_double * 3)]
+    bh = ref_black_hole(1.0, 0.0)
+    dk = abi.disk(6.0, 20.0, 1.0, 1.0)
+    cfg = abi.sim_config(0.1, 100.0, 1000, 1e-6)
+    W, H = 24, 16
+    rows = []
+    REF.quiet(1)
+    for camname in ("A", "B", "V"):
+        cam = configs.camera(camname)
+        for py in range(0, H, 3):
+            for px in range(0, W, 3):
+                col = (C.c_double * 3)()
+                res = L.trace_pixel(px, py, W, H, C.byref(cam.position), C.byref(cam.direction),
+                                    C.byref(cam.up), cam.fov_deg, C.byref(bh), C.byref(dk),
+                                    C.byref(cfg), None, None, C.byref(col))
+                c = list(col) if res != abi.RAY_DISK else [np.nan] * 3
+                rows.append([ord(camname), px, py, res] + c)
+    REF.quiet(0)
+    save("trace_pixel", W=np.array(W), H=np.array(H), rows=np.array(rows))
+
+
+def paths():
+    """integrate_photon_path with a recorded path (raytracer.c:338-679)."""
+    L.integrate_photon_path.argtypes = [P(abi.Vector4D), P(abi.Vector3D), P(abi.BlackHoleParams),
+                                        P(abi.SimulationConfig), C.c_int, C.c_void_p, C.c_int,
+                                        P(C.c_int), P(abi.RayTraceHit)]
+    cases = [  # origin4, dir, spin, method, max_steps, max_positions
+        ((0, 0, 0, 30), (0.3, 0, -1), 0.0, abi.INTEGRATOR_RK4, 200, 64),
+        ((0, 0, 0, 30), (0.3, 0, -1), 0.0, abi.INTEGRATOR_RKF45, 200, 300),
+        ((2.5, 30, 0, 0), (-1, 0, 0.1), 0.0, abi.INTEGRATOR_RK4, 120, 200),
+        ((0, 0, -29.544, 5.209), (0.1, 29.544, -5.209), 0.99, abi.INTEGRATOR_RKF45, 2000, 100),
+        ((0, 10, 0, 0), (0, 1, 0), 0.0, abi.INTEGRATOR_LEAPFROG, 30, 40),
+        ((0, 0, 0, 1.5), (1, 0, 0), 0.0, abi.INTEGRATOR_RK4, 50, 10),
+        ((0, 0, 0, 30), (0.3, 0, -1), 0.0, abi.INTEGRATOR_RK4, 60, 0),
+    ]
+    out = {}
+    REF.quiet(1)
+    for i, (o4, d3, spin, method, steps, maxp) in enumerate(cases):
+        bh = ref_black_hole(1.0, spin)
+        cfg = abi.sim_config(0.1, 100.0, steps, 1e-6 if spin == 0 else 1e-8)
+        path = (abi.Vector3D * max(maxp, 1))()
+        num = C.c_int(0)
+        hit = abi.RayTraceHit()
+        res = L.integrate_photon_path(C.byref(abi.Vector4D(*o4)), C.byref(abi.v3(*d3)),
+                                      C.byref(bh), C.byref(cfg), method,
+                                      C.cast(path, C.c_void_p), maxp, C.byref(num),
+                                      C.byref(hit))
+        n = num.value
+        out[f"case{i}_in"] = np.array(list(o4) + list(d3) + [spin, method, steps, maxp])
+        out[f"case{i}_res"] = np.array([res, n, hit.result, hit.steps])
+        out[f"case{i}_hit"] = np.array([hit.hit_position.x, hit.hit_position.y,
+                                        hit.hit_position.z, hit.distance, hit.time_dilation,
+                                        hit.sky_direction.x, hit.sky_direction.y,
+                                        hit.sky_direction.z])
+        stored = max(0, min(n, maxp))
+        out[f"case{i}_path"] = np.array([[p.x, p.y, p.z] for p in path[:stored]]).reshape(-1, 3)
+    REF.quiet(0)
+    out["ncases"] = np.array(len(cases))
+    save("paths", **out)
+
+
+if __name__ == "__main__":
+    kat_main()
+    shading()
+    pixels()
+    paths()
+    edge_rays()
+    frames()
