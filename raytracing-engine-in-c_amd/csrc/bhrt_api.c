@@ -444,15 +444,18 @@ typedef struct {
 static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_rows* rows) {
     devctx_t* c = j->c;
     HIP_TRY(hipSetDevice(c->device));
+    /* only the fields the caller asked for (the device may hold extra ones, e.g. the hit
+     * point the colour pass reads) */
+#define WANTED(f) (*soa_slot(&j->dev, f) && *soa_slot((bhrt_frame_soa*)host, f))
     size_t bytes = 0;
     for (int f = 0; f < BHRT_NFIELDS; f++)
-        if (*soa_slot(&j->dev, f)) bytes += k_fsize[f] * (size_t)j->n;
+        if (WANTED(f)) bytes += k_fsize[f] * (size_t)j->n;
     if (ensure(&c->h_stage, &c->cap_stage, bytes ? bytes : 64, 1)) return -1;
     char* stage = (char*)c->h_stage;
     size_t off = 0;
     for (int f = 0; f < BHRT_NFIELDS; f++) {
         void* src = *soa_slot(&j->dev, f);
-        if (!src) continue;
+        if (!WANTED(f)) continue;
         HIP_TRY(hipMemcpyAsync(stage + off, src, k_fsize[f] * (size_t)j->n,
                                hipMemcpyDeviceToHost, c->stream));
         off += k_fsize[f] * (size_t)j->n;
@@ -460,8 +463,7 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
     HIP_TRY(hipStreamSynchronize(c->stream));
     off = 0;
     for (int f = 0; f < BHRT_NFIELDS; f++) {
-        void* src = *soa_slot(&j->dev, f);
-        if (!src) continue;
+        if (!WANTED(f)) continue;
         char* dst = (char*)*soa_slot((bhrt_frame_soa*)host, f);
         size_t fs = k_fsize[f];
         if (!rows || rows->num_shards <= 1) {
@@ -476,6 +478,7 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
         }
         off += fs * (size_t)j->n;
     }
+#undef WANTED
     return 0;
 }
 
