@@ -370,11 +370,15 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
         set_err("rgb output needs rgb_r/g/b, result and hit_x/hit_y");
         return -1;
     }
+    if (ensure(&c->d_init, &c->cap_init,
+               (size_t)BHRT_INIT_FIELDS * sizeof(double) * (size_t)nrows * (size_t)W, 0))
+        return -1;
     bhrt_kparams kp;
     fill_scene(&kp, bh, dk, cfg, method, flags);
     fill_camera(&kp, cam, W, H);
     if (rows && rows->num_shards > 1) kp.cam.rows = *rows;
     kp.n = nrows * W;
+    kp.init = (double*)c->d_init;
     kp.out = *out;
     return launch(c, &kp, (hipStream_t)stream);
 }

@@ -47,6 +47,30 @@ struct Counters {
     unsigned rays = 0, iters = 0, full = 0, far_ = 0, kerr = 0;
 };
 
+// IEEE-exact division without the generic fdiv scaffolding.
+// rcp_nr is the reciprocal refinement the compiler's f64 fdiv performs after v_div_scale
+// (v_rcp_f64 + two Newton steps); div_nr is its quotient step (q = a*y, one FMA residual,
+// one FMA correction). For operands in the normal range v_div_scale is the identity, so
+// div_nr(a, b, rcp_nr(b)) is bit-identical to a / b -- and one reciprocal serves every
+// quotient with the same divisor. Callers keep the IEEE a / b for out-of-range operands.
+__device__ __forceinline__ double rcp_nr(double b) {
+    double y = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-b, y, 1.0);
+    return __builtin_fma(y, e, y);
+}
+__device__ __forceinline__ double div_nr(double a, double b, double yb) {
+    const double q = a * yb;
+    return __builtin_fma(__builtin_fma(-b, q, a), yb, q);
+}
+// a / 6.0, correctly rounded: RN(1/6) is the exact reciprocal's rounding (Markstein).
+__device__ __forceinline__ double div6(double a) {
+    constexpr double y = 1.0 / 6.0;
+    const double q = a * y;
+    return __builtin_fma(__builtin_fma(-6.0, q, a), y, q);
+}
+
 // ray_derivatives (raytracer.c:44-154). y = (t, r, theta, phi, tdot, rdot) of the caller,
 // read -- as the reference does -- as (r, theta, phi, v_r, v_theta, v_phi).
 template <bool SPIN0>
@@ -76,13 +100,27 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
             st = (st >= 0.0) ? 0.01 : -0.01;
             st2 = st * st;
         }
-        const double f = 1.0 - sc.rs / r;
-        const double term1 = -sc.M / (rsq * f) * f;
         const double term2 = r * y[4] * y[4];
         const double term3 = r * st2 * y[5] * y[5];
-        d[3] = term1 + term2 + term3;
-        d[4] = -2.0 * y[3] * y[4] / r + st * ct * y[5] * y[5];
-        d[5] = -2.0 * y[3] * y[5] / r - 2.0 * y[4] * y[5] * ct / st;
+        const double n4 = -2.0 * y[3] * y[4];
+        const double n5a = -2.0 * y[3] * y[5];
+        const double n5b = 2.0 * y[4] * y[5] * ct;
+        const double sc4 = st * ct * y[5] * y[5];
+        if (r < 1.0e150) {  // r >= 1.5 rs here: every divisor is in the normal range
+            const double yr = rcp_nr(r);
+            const double f = 1.0 - div_nr(sc.rs, r, yr);
+            const double den = rsq * f;
+            const double term1 = -div_nr(sc.M, den, rcp_nr(den)) * f;
+            d[3] = term1 + term2 + term3;
+            d[4] = div_nr(n4, r, yr) + sc4;
+            d[5] = div_nr(n5a, r, yr) - div_nr(n5b, st, rcp_nr(st));
+        } else {
+            const double f = 1.0 - sc.rs / r;
+            const double term1 = -sc.M / (rsq * f) * f;
+            d[3] = term1 + term2 + term3;
+            d[4] = n4 / r + sc4;
+            d[5] = n5a / r - n5b / st;
+        }
         n.full++;
     } else {  // :131-138
         d[3] = 0.0;
@@ -90,12 +128,17 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         d[5] = 0.0;
         n.kerr++;
     }
+    // :141-153 -- non-finite -> 0 for all six, then |d[3..5]| <= 10. One combined test;
+    // the per-component repair runs only when some lane actually holds an Inf/NaN.
+    const int finite = (int)isfinite(d[0]) & (int)isfinite(d[1]) & (int)isfinite(d[2]) &
+                       (int)isfinite(d[3]) & (int)isfinite(d[4]) & (int)isfinite(d[5]);
+    if (!finite) {
 #pragma unroll
-    for (int i = 0; i < 6; i++)  // :141-145
-        if (!isfinite(d[i])) d[i] = 0.0;
+        for (int i = 0; i < 6; i++)
+            if (!isfinite(d[i])) d[i] = 0.0;
+    }
 #pragma unroll
-    for (int i = 3; i < 6; i++)  // :148-153
-        if (fabs(d[i]) > 10.0) d[i] = (d[i] > 0.0) ? 10.0 : -10.0;
+    for (int i = 3; i < 6; i++) d[i] = fmin(fmax(d[i], -10.0), 10.0);
 }
 
 // rk4_integrate (math_util.c:162-207) on the six live components; the running sum
@@ -125,7 +168,7 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
     }
     rhs<SPIN0>(yt, k, sc, far_ok, n);
 #pragma unroll
-    for (int i = 0; i < 6; i++) y[i] += h * (acc[i] + k[i]) / 6.0;
+    for (int i = 0; i < 6; i++) y[i] += div6(h * (acc[i] + k[i]));
 }
 
 // rkf45_integrate (math_util.c:212-457), n = 6. Returns true on accept (y <- y5).
@@ -327,7 +370,8 @@ __device__ __forceinline__ bool disk_test(Ray_& R, double nx, double ny, double 
                                           const Scene& sc) {
     const double den = (R.dx * nx + R.dy * ny) + R.dz * nz;
     if (fabs(den) < kEps) return false;
-    const double t = -((R.px * nx + R.py * ny) + R.pz * nz) / den;
+    const double num = -((R.px * nx + R.py * ny) + R.pz * nz);
+    const double t = fabs(den) < 1.0e150 ? div_nr(num, den, rcp_nr(den)) : num / den;
     if (t < 0.0) return false;
     const double qx = R.px + R.dx * t, qy = R.py + R.dy * t, qz = R.pz + R.dz * t;
     const double rxy = sqrt(qx * qx + qy * qy);
@@ -455,13 +499,20 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
     return s;
 }
 
-// Set-up of an array of rays with arbitrary origins: [BHRT_INIT_FIELDS][n] state table.
-__global__ __launch_bounds__(256) void k_init_rays(const bhrt_kparams kp) {
+// Per-ray set-up pass (integrate_photon_path's prologue, raytracer.c:355-507) into the
+// [BHRT_INIT_FIELDS][n] state table the trace kernel refills from. Kept out of the
+// persistent loop so that neither the camera uniforms nor acos/atan2 occupy registers there.
+template <int SRC>
+__global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += gridDim.x * blockDim.x) {
-        const Ray ray = kp.rays[i];
         Ray_ R;
-        ray_init_general(R, 0.0, ray.origin.x, ray.origin.y, ray.origin.z, ray.direction.x,
-                         ray.direction.y, ray.direction.z, kp.sc);
+        if (SRC == BHRT_SRC_CAMERA) {
+            ray_init_camera(R, kp.cam, i);
+        } else {
+            const Ray ray = kp.rays[i];
+            ray_init_general(R, 0.0, ray.origin.x, ray.origin.y, ray.origin.z, ray.direction.x,
+                             ray.direction.y, ray.direction.z, kp.sc);
+        }
         double* f = kp.init;
         const long n = kp.n;
 #pragma unroll
@@ -480,7 +531,7 @@ __global__ __launch_bounds__(256) void k_init_rays(const bhrt_kparams kp) {
 
 // Persistent trace kernel: grid = what is resident; each wave refills idle lanes from the
 // global queue kp.ctl[0] (one returning atomic per refill).
-template <int METHOD, bool DISK, int SRC, bool SPIN0>
+template <int METHOD, bool DISK, bool SPIN0>
 __global__ __launch_bounds__(256) void k_trace(const bhrt_kparams kp) {
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
@@ -502,8 +553,7 @@ __global__ __launch_bounds__(256) void k_trace(const bhrt_kparams kp) {
                 const unsigned long long id = base + __popcll(~live_mask & below);
                 if (id < (unsigned long long)kp.n) {
                     rid = (int)id;
-                    if (SRC == BHRT_SRC_CAMERA) ray_init_camera(R, kp.cam, rid);
-                    else load_init(kp, rid, R);
+                    load_init(kp, rid, R);
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
@@ -662,46 +712,44 @@ int grid_for(const void* fn, int n) {
     return blocks < 1 ? 1 : (int)blocks;
 }
 
-template <int METHOD, bool DISK, int SRC, bool SPIN0>
+template <int METHOD, bool DISK, bool SPIN0>
 int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     static int grid_cap = 0;  // resident workgroups for this instantiation
     if (grid_cap == 0)
-        grid_cap = grid_for(reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SRC, SPIN0>),
-                            1 << 30);
-    if (SRC == BHRT_SRC_RAYS) {
-        const int g = grid_for(reinterpret_cast<const void*>(&k_init_rays), kp.n);
-        k_init_rays<<<g, 256, 0, st>>>(kp);
-    }
+        grid_cap = grid_for(reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0>), 1 << 30);
+    if (kp.src == BHRT_SRC_CAMERA)
+        k_init<BHRT_SRC_CAMERA><<<grid_for(reinterpret_cast<const void*>(&k_init<BHRT_SRC_CAMERA>),
+                                           kp.n), 256, 0, st>>>(kp);
+    else
+        k_init<BHRT_SRC_RAYS><<<grid_for(reinterpret_cast<const void*>(&k_init<BHRT_SRC_RAYS>),
+                                         kp.n), 256, 0, st>>>(kp);
     int blocks = (kp.n + 255) / 256;
     if (blocks > grid_cap) blocks = grid_cap;
     if (blocks < 1) blocks = 1;
     if (ev0) (void)hipEventRecord(ev0, st);
-    k_trace<METHOD, DISK, SRC, SPIN0><<<blocks, 256, 0, st>>>(kp);
+    k_trace<METHOD, DISK, SPIN0><<<blocks, 256, 0, st>>>(kp);
     if (ev1) (void)hipEventRecord(ev1, st);
     if (kp.out.rgb_r) {
-        const int g = grid_for(reinterpret_cast<const void*>(&k_colour<SRC>), kp.n);
-        k_colour<SRC><<<g, 256, 0, st>>>(kp);
+        if (kp.src == BHRT_SRC_CAMERA)
+            k_colour<BHRT_SRC_CAMERA><<<grid_for(reinterpret_cast<const void*>(&k_colour<BHRT_SRC_CAMERA>),
+                                                 kp.n), 256, 0, st>>>(kp);
+        else
+            k_colour<BHRT_SRC_RAYS><<<grid_for(reinterpret_cast<const void*>(&k_colour<BHRT_SRC_RAYS>),
+                                               kp.n), 256, 0, st>>>(kp);
     }
     return (int)hipGetLastError();
 }
 
-template <int METHOD, bool DISK, int SRC>
-int dispatch_spin(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-    return kp.sc.spin0 ? launch_t<METHOD, DISK, SRC, true>(kp, st, e0, e1)
-                       : launch_t<METHOD, DISK, SRC, false>(kp, st, e0, e1);
-}
-
 template <int METHOD, bool DISK>
-int dispatch_src(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-    return kp.src == BHRT_SRC_CAMERA
-               ? dispatch_spin<METHOD, DISK, BHRT_SRC_CAMERA>(kp, st, e0, e1)
-               : dispatch_spin<METHOD, DISK, BHRT_SRC_RAYS>(kp, st, e0, e1);
+int dispatch_spin(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+    return kp.sc.spin0 ? launch_t<METHOD, DISK, true>(kp, st, e0, e1)
+                       : launch_t<METHOD, DISK, false>(kp, st, e0, e1);
 }
 
 template <int METHOD>
 int dispatch_disk(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-    return kp.sc.has_disk ? dispatch_src<METHOD, true>(kp, st, e0, e1)
-                          : dispatch_src<METHOD, false>(kp, st, e0, e1);
+    return kp.sc.has_disk ? dispatch_spin<METHOD, true>(kp, st, e0, e1)
+                          : dispatch_spin<METHOD, false>(kp, st, e0, e1);
 }
 
 template <int METHOD>
