@@ -28,7 +28,7 @@
 #include "bhrt_kernel.h"
 
 #ifndef BHRT_CONTRACT
-#define BHRT_CONTRACT 0
+#define BHRT_CONTRACT 1
 #endif
 #if BHRT_CONTRACT
 #pragma clang fp contract(fast)
@@ -71,15 +71,103 @@ __device__ __forceinline__ double div6(double a) {
     return __builtin_fma(__builtin_fma(-6.0, q, a), y, q);
 }
 
+// sin and cos of one argument, for the trace loop. OCML's sincos
+// spends ~78 VALU per call on a range reduction valid to 2^30+; every argument here (the
+// radius read as an angle by ray_derivatives, theta, phi) stays far below 2^20, where a
+// three-constant Cody-Waite reduction with FMA is exact up to a double-double tail. The
+// tail feeds the fdlibm kernels (k_sin.c / k_cos.c, FreeBSD form). Measured on 6e7 random
+// arguments against glibc (the reference's libm): max 1 ulp, 97% bit-identical.
+// |x| >= 2^20, Inf and NaN take OCML's sincos (not inlined: its Payne-Hanek path must not
+// cost registers in the loop).
+__device__ __attribute__((noinline)) void sincos_ocml(double x, double* s, double* c) {
+    sincos(x, s, c);
+}
+
+__device__ __forceinline__ void bhrt_sincos(double x, double* so, double* co) {
+    if (!(fabs(x) < 1048576.0)) {
+        sincos_ocml(x, so, co);
+        return;
+    }
+    constexpr double kTwoOverPi = 6.36619772367581382433e-01;
+    constexpr double P1 = 1.57079632679489655800e+00;   // pi/2 in three parts
+    constexpr double P2 = 6.12323399573676603587e-17;
+    constexpr double P3 = -1.49738490485916983e-33;
+    const double n = rint(x * kTwoOverPi);
+    const double r1 = __builtin_fma(-n, P1, x);          // exact for |x| < 2^20
+    const double p2 = n * P2;
+    const double p2e = __builtin_fma(n, P2, -p2);        // n*P2 = p2 + p2e exactly
+    const double hi = r1 - p2;                           // TwoSum(r1, -p2)
+    const double t = hi - r1;
+    const double e = (r1 - (hi - t)) - (p2 + t);
+    const double lo = __builtin_fma(-n, P3, e - p2e);
+    const double r = hi + lo;                            // reduced argument r + y
+    const double y = (hi - r) + lo;
+    constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                     S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                     S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                     C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                     C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double z = r * r, w = z * z;
+    const double rs_ = __builtin_fma(z, __builtin_fma(z, S4, S3), S2) +
+                       z * w * __builtin_fma(z, S6, S5);
+    const double v = z * r;
+    const double s = r - ((z * (0.5 * y - v * rs_) - y) - v * S1);
+    const double rc = z * __builtin_fma(z, __builtin_fma(z, C3, C2), C1) +
+                      w * w * __builtin_fma(z, __builtin_fma(z, C6, C5), C4);
+    const double hz = 0.5 * z, ww = 1.0 - hz;
+    const double c = ww + (((1.0 - ww) - hz) + (z * rc - r * y));
+    const int q = (int)n;
+    double ss = (q & 1) ? c : s;
+    double cc = (q & 1) ? s : c;
+    *so = (q & 2) ? -ss : ss;
+    *co = ((q + 1) & 2) ? -cc : cc;
+}
+
+// sin and cos of a + delta from s0 = sin(a), c0 = cos(a). Every
+// RK4/RKF45 stage after the first evaluates ray_derivatives at theta = y1 + delta with a
+// small delta (the stage increment of state[1]; |delta| < 0.09 on a full C2 frame), so one
+// direct sincos per iteration serves all stages: sin(delta) and cos(delta) - 1 come from
+// the fdlibm k_sin / k_cos polynomials and the shift adds only small corrections to s0, c0
+// (error <= the direct value's + 0.5 ulp). Returns false, leaving the outputs unset, when
+// delta is outside [-pi/4, pi/4] or when a + delta - a would not be exact; the caller then
+// evaluates sincos directly.
+__device__ __forceinline__ bool sincos_shift(double a, double s0, double c0, double x, double& s,
+                                             double& c) {
+    const double delta = x - a;  // exact when x in [a/2, 2a] (Sterbenz)
+    if (!(fabs(delta) <= 0.78539816339744828 && fabs(delta) <= 0.5 * fabs(a))) return false;
+    constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                     S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                     S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                     C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                     C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double z = delta * delta, w = z * z;
+    const double r = __builtin_fma(z, __builtin_fma(z, S4, S3), S2) +
+                     z * w * __builtin_fma(z, S6, S5);
+    const double sd = delta + (z * delta) * (S1 + z * r);           // k_sin, tail 0
+    const double rc = z * __builtin_fma(z, __builtin_fma(z, C3, C2), C1) +
+                      w * w * __builtin_fma(z, __builtin_fma(z, C6, C5), C4);
+    const double cm1 = z * rc - 0.5 * z;                             // k_cos - 1
+    s = s0 + (s0 * cm1 + c0 * sd);
+    c = c0 + (c0 * cm1 - s0 * sd);
+    return true;
+}
+
 // ray_derivatives (raytracer.c:44-154). y = (t, r, theta, phi, tdot, rdot) of the caller,
 // read -- as the reference does -- as (r, theta, phi, v_r, v_theta, v_phi).
-template <bool SPIN0>
+// Trig of theta (= y[1]) for one RK stage: stage 1 evaluates it, later stages shift it.
+struct Trig1 {
+    double a = __builtin_nan(""), s = 0.0, c = 0.0;  // theta of stage 1 and its sin, cos;
+};                                                   // NaN until stage 1 evaluated them
+
+template <bool SPIN0, bool FAR>
 __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const Scene& sc,
-                                    bool far_ok, Counters& n) {
+                                    bool far_ok, Counters& n, Trig1& tr, bool first) {
     d[0] = y[3];
     d[1] = y[4];
     d[2] = y[5];
-    if (far_ok && y[0] > sc.rs_x15) {  // weak-field branch, no NaN/clamp pass (:65-86)
+    if (FAR && far_ok && y[0] > sc.rs_x15) {  // weak-field branch, no NaN/clamp pass (:65-86)
         d[3] = 0.0;
         d[4] = 0.0;
         d[5] = y[5] * (sc.two_m / (y[0] * y[0]));
@@ -90,7 +178,14 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         double r = y[0];
         double rsq = r * r;
         double st, ct;
-        sincos(y[1], &st, &ct);
+        if (first) {
+            bhrt_sincos(y[1], &st, &ct);
+            tr.a = y[1];
+            tr.s = st;
+            tr.c = ct;
+        } else if (!sincos_shift(tr.a, tr.s, tr.c, y[1], st, ct)) {
+            bhrt_sincos(y[1], &st, &ct);
+        }
         double st2 = st * st;
         if (r <= sc.rs_x1_5) {
             r = sc.rs_x1_5;
@@ -143,36 +238,37 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
 
 // rk4_integrate (math_util.c:162-207) on the six live components; the running sum
 // ((k1 + 2k2) + 2k3) + k4 is the reference's left-to-right evaluation order.
-template <bool SPIN0>
+template <bool SPIN0, bool FAR>
 __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& sc, bool far_ok,
                                          Counters& n) {
     double k[6], acc[6], yt[6];
     const double hh = 0.5 * h;
-    rhs<SPIN0>(y, k, sc, far_ok, n);
+    Trig1 tr;
+    rhs<SPIN0, FAR>(y, k, sc, far_ok, n, tr, true);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         acc[i] = k[i];
         yt[i] = y[i] + hh * k[i];
     }
-    rhs<SPIN0>(yt, k, sc, far_ok, n);
+    rhs<SPIN0, FAR>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         acc[i] = acc[i] + 2.0 * k[i];
         yt[i] = y[i] + hh * k[i];
     }
-    rhs<SPIN0>(yt, k, sc, far_ok, n);
+    rhs<SPIN0, FAR>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         acc[i] = acc[i] + 2.0 * k[i];
         yt[i] = y[i] + h * k[i];
     }
-    rhs<SPIN0>(yt, k, sc, far_ok, n);
+    rhs<SPIN0, FAR>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) y[i] += div6(h * (acc[i] + k[i]));
 }
 
 // rkf45_integrate (math_util.c:212-457), n = 6. Returns true on accept (y <- y5).
-template <bool SPIN0>
+template <bool SPIN0, bool FAR>
 __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Scene& sc,
                                               bool far_ok, Counters& n) {
     constexpr double b21 = 1.0 / 4.0;
@@ -187,7 +283,8 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
     constexpr double d1 = 16.0 / 135.0, d3 = 6656.0 / 12825.0, d4 = 28561.0 / 56430.0,
                      d5 = -9.0 / 50.0, d6 = 2.0 / 55.0;
     double k1[6], k2[6], k3[6], k4[6], k5[6], k6[6], yt[6];
-    rhs<SPIN0>(y, k1, sc, far_ok, n);
+    Trig1 tr;
+    rhs<SPIN0, FAR>(y, k1, sc, far_ok, n, tr, true);
     bool bad = false;
 #pragma unroll
     for (int i = 0; i < 6; i++) bad |= !isfinite(k1[i]);  // :318-333
@@ -195,21 +292,21 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
     const double hb21 = h * b21;
 #pragma unroll
     for (int i = 0; i < 6; i++) yt[i] = y[i] + hb21 * k1[i];
-    rhs<SPIN0>(yt, k2, sc, far_ok, n);
+    rhs<SPIN0, FAR>(yt, k2, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) yt[i] = y[i] + h * (b31 * k1[i] + b32 * k2[i]);
-    rhs<SPIN0>(yt, k3, sc, far_ok, n);
+    rhs<SPIN0, FAR>(yt, k3, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) yt[i] = y[i] + h * (b41 * k1[i] + b42 * k2[i] + b43 * k3[i]);
-    rhs<SPIN0>(yt, k4, sc, far_ok, n);
+    rhs<SPIN0, FAR>(yt, k4, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++)
         yt[i] = y[i] + h * (b51 * k1[i] + b52 * k2[i] + b53 * k3[i] + b54 * k4[i]);
-    rhs<SPIN0>(yt, k5, sc, far_ok, n);
+    rhs<SPIN0, FAR>(yt, k5, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++)
         yt[i] = y[i] + h * (b61 * k1[i] + b62 * k2[i] + b63 * k3[i] + b64 * k4[i] + b65 * k5[i]);
-    rhs<SPIN0>(yt, k6, sc, far_ok, n);
+    rhs<SPIN0, FAR>(yt, k6, sc, far_ok, n, tr, false);
     double y5[6];
     double max_error = 0.0;
 #pragma unroll
@@ -232,8 +329,8 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
 __device__ __forceinline__ void sph2cart(double r, double th, double ph, double& x, double& y,
                                          double& z) {
     double st, ct, sp, cp;
-    sincos(th, &st, &ct);
-    sincos(ph, &sp, &cp);
+    bhrt_sincos(th, &st, &ct);
+    bhrt_sincos(ph, &sp, &cp);
     x = r * st * cp;
     y = r * st * sp;
     z = r * ct;
@@ -388,7 +485,7 @@ enum Term : int { T_NONE = 0, T_HORIZON, T_DISK, T_MAXDIST, T_MAXSTEPS };
 
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
 // on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
-template <int METHOD, bool DISK, bool SPIN0>
+template <int METHOD, bool DISK, bool SPIN0, bool FAR>
 __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n) {
 #pragma unroll
     for (int i = 0; i < 6; i++)  // :543-548
@@ -403,9 +500,9 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     bool moved = true;
     n.iters++;
     if (METHOD == INTEGRATOR_RK4) {
-        rk4_step<SPIN0>(R.y, h, sc, R.far_ok, n);
+        rk4_step<SPIN0, FAR>(R.y, h, sc, R.far_ok, n);
     } else if (METHOD == INTEGRATOR_RKF45) {
-        moved = rkf45_attempt<SPIN0>(R.y, h, sc, R.far_ok, n);
+        moved = rkf45_attempt<SPIN0, FAR>(R.y, h, sc, R.far_ok, n);
     } else {
         moved = false;  // LEAPFROG / YOSHIDA: "not implemented", state unchanged (:616-624)
     }
@@ -531,8 +628,19 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 
 // Persistent trace kernel: grid = what is resident; each wave refills idle lanes from the
 // global queue kp.ctl[0] (one returning atomic per refill).
-template <int METHOD, bool DISK, bool SPIN0>
-__global__ __launch_bounds__(256) void k_trace(const bhrt_kparams kp) {
+#ifndef BHRT_WAVES_PER_EU
+#define BHRT_WAVES_PER_EU 0
+#endif
+#if BHRT_WAVES_PER_EU > 0
+#define BHRT_TRACE_BOUNDS __launch_bounds__(256, BHRT_WAVES_PER_EU)
+#else
+#define BHRT_TRACE_BOUNDS __launch_bounds__(256)
+#endif
+
+// FAR: some ray may take ray_derivatives' weak-field branch (origin beyond 15 rs). A camera
+// frame knows this once for all its rays (shared origin); ray arrays always assume it.
+template <int METHOD, bool DISK, bool SPIN0, bool FAR>
+__global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
     Counters n;
@@ -569,7 +677,7 @@ __global__ __launch_bounds__(256) void k_trace(const bhrt_kparams kp) {
             continue;
         }
         if (live) {
-            const int term = ray_iterate<METHOD, DISK, SPIN0>(R, kp.sc, n);
+            const int term = ray_iterate<METHOD, DISK, SPIN0, FAR>(R, kp.sc, n);
             if (term != T_NONE) {
                 store_hit(kp.out, rid, R, term, kp.sc);
                 live = false;
@@ -679,7 +787,7 @@ __global__ void k_path(const bhrt_kparams kp, double t0, double ox, double oy, d
     if (kp.sc.max_steps > 0) {
         for (;;) {
             const int k_before = R.k;
-            term = ray_iterate<METHOD, false, SPIN0>(R, kp.sc, n);
+            term = ray_iterate<METHOD, false, SPIN0, true>(R, kp.sc, n);
             // positions of the iterations executed (a fixed-point jump repeats p_k)
             for (int j = k_before; j < R.k && path && num >= 0 && num < max_positions; j++) {
                 path[num].x = R.px;
@@ -712,11 +820,12 @@ int grid_for(const void* fn, int n) {
     return blocks < 1 ? 1 : (int)blocks;
 }
 
-template <int METHOD, bool DISK, bool SPIN0>
+template <int METHOD, bool DISK, bool SPIN0, bool FAR>
 int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     static int grid_cap = 0;  // resident workgroups for this instantiation
     if (grid_cap == 0)
-        grid_cap = grid_for(reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0>), 1 << 30);
+        grid_cap = grid_for(reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR>),
+                            1 << 30);
     if (kp.src == BHRT_SRC_CAMERA)
         k_init<BHRT_SRC_CAMERA><<<grid_for(reinterpret_cast<const void*>(&k_init<BHRT_SRC_CAMERA>),
                                            kp.n), 256, 0, st>>>(kp);
@@ -727,7 +836,7 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
     if (blocks > grid_cap) blocks = grid_cap;
     if (blocks < 1) blocks = 1;
     if (ev0) (void)hipEventRecord(ev0, st);
-    k_trace<METHOD, DISK, SPIN0><<<blocks, 256, 0, st>>>(kp);
+    k_trace<METHOD, DISK, SPIN0, FAR><<<blocks, 256, 0, st>>>(kp);
     if (ev1) (void)hipEventRecord(ev1, st);
     if (kp.out.rgb_r) {
         if (kp.src == BHRT_SRC_CAMERA)
@@ -740,10 +849,17 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
     return (int)hipGetLastError();
 }
 
+template <int METHOD, bool DISK, bool SPIN0>
+int dispatch_far(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+    const bool far = kp.src != BHRT_SRC_CAMERA || kp.cam.use_approx;
+    return far ? launch_t<METHOD, DISK, SPIN0, true>(kp, st, e0, e1)
+               : launch_t<METHOD, DISK, SPIN0, false>(kp, st, e0, e1);
+}
+
 template <int METHOD, bool DISK>
 int dispatch_spin(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-    return kp.sc.spin0 ? launch_t<METHOD, DISK, true>(kp, st, e0, e1)
-                       : launch_t<METHOD, DISK, false>(kp, st, e0, e1);
+    return kp.sc.spin0 ? dispatch_far<METHOD, DISK, true>(kp, st, e0, e1)
+                       : dispatch_far<METHOD, DISK, false>(kp, st, e0, e1);
 }
 
 template <int METHOD>
