@@ -32,12 +32,12 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from bhrt import abi, configs, lib  # noqa: E402
+from bhrt.dist_frame import FrameBuffer, gather_frame  # noqa: E402
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (and FP64 matrix) peak, AMD spec
 METRIC = "Mrays/s (and RK4 steps/s) per GPU + per node; max |Δhit| vs CPU ref"
 ROW_BLOCK = 8
 FIELDS = abi.SOA_FIELDS
-INT_FIELDS = ("result", "steps")
 
 
 def parse():
@@ -57,21 +57,6 @@ def parse():
 def flops(st, method):
     per_iter = 368 if method == abi.INTEGRATOR_RKF45 else 117
     return per_iter * st["iterations"] + 35 * st["stages_full"] + 4 * st["stages_far"]
-
-
-class Frame:
-    """Device SoA of one shard, carved from ONE byte buffer so the gather is one collective."""
-
-    def __init__(self, n, device):
-        self.n = n
-        sizes = [4 if f in INT_FIELDS else 8 for f in FIELDS]
-        self.offsets = np.concatenate([[0], np.cumsum([s * n for s in sizes])]).astype(int)
-        self.buf = torch.empty(int(self.offsets[-1]), dtype=torch.uint8, device=device)
-        self.views = {}
-        for i, f in enumerate(FIELDS):
-            dt = torch.int32 if f in INT_FIELDS else torch.float64
-            self.views[f] = self.buf[self.offsets[i]:self.offsets[i + 1]].view(dt)
-        self.soa = lib.soa_from_tensors(self.views)
 
 
 def main():
@@ -97,25 +82,16 @@ def main():
     rows = abi.Rows(ROW_BLOCK, rank, world)
     n_rows = lib.shard_rows(H, rows)
     n = n_rows * W
-    frame = Frame(n, device)
+    frame = FrameBuffer(n, device)
+    soa = frame.soa()
     stream = torch.cuda.current_stream()
     gathered = [torch.empty_like(frame.buf) for _ in range(world)] if (world > 1 and rank == 0) else None
 
     def step():
         lib.render_frame_device(bh, dk, cfg, cam, W, H, rows if world > 1 else None, c.method,
-                                c.flags, frame.soa, stream.cuda_stream)
-        if world > 1:
-            dist.gather(frame.buf, gathered, dst=0)
-            if rank == 0:  # un-permute cyclic row blocks into the H x W image
-                img = {}
-                for i, f in enumerate(FIELDS):
-                    dt = torch.int32 if f in INT_FIELDS else torch.float64
-                    parts = torch.stack([g[frame.offsets[i]:frame.offsets[i + 1]].view(dt)
-                                         for g in gathered])
-                    img[f] = (parts.view(world, n_rows // ROW_BLOCK, ROW_BLOCK, W)
-                              .permute(1, 0, 2, 3).reshape(H, W))
-                return img
-        return None
+                                c.flags, soa, stream.cuda_stream)
+        # one RCCL gather of the packed shards + un-permute into the H x W image on rank 0
+        return gather_frame(frame, H, W, ROW_BLOCK, world, rank, gathered)
 
     for _ in range(args.warmup):
         step()

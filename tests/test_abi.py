@@ -176,3 +176,19 @@ def test_no_cpu_fallback_without_gpu():
     with pytest.raises(lib.BhrtError):
         lib.render_frame(bh, None, cfg, abi.Camera(abi.v3(0, 0, 30), abi.v3(0, 0, -1),
                                                    abi.v3(0, 1, 0), 60.0), 4, 4)
+
+
+def build_c_demo(tmp_path):
+    """Compile examples/trace_demo.c, a C caller written against the reference's header
+    names (include/blackhole_api.h etc. forward to bhrt_api.h), and link it to libbhrt.so."""
+    import subprocess
+    exe = str(tmp_path / "trace_demo")
+    libdir = os.path.dirname(lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "examples", "trace_demo.c"), "-L", libdir, "-lbhrt",
+                    f"-Wl,-rpath,{libdir}", "-lm", "-o", exe], check=True)
+    return exe
+
+
+def test_c_demo_links_against_drop_in_headers(tmp_path):
+    assert os.path.exists(build_c_demo(tmp_path))

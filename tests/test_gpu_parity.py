@@ -261,3 +261,19 @@ def test_empty_and_degenerate_inputs(bhrt_lib):
     assert rc == -1
     one = bhrt_lib.render_frame(bh, None, cfg, configs.camera("A"), 1, 1)
     assert one["result"][0] == abi.RAY_MAX_STEPS
+
+
+def test_c_caller_drop_in(bhrt_lib, tmp_path):
+    """A plain C program using the reference API (bh_* + trace batch) gets main.c's known
+    answers from libbhrt.so."""
+    import subprocess
+    from test_abi import build_c_demo
+    out = subprocess.run([build_c_demo(tmp_path)], check=True, capture_output=True, text=True).stdout
+    g = golden("kat_main5")
+    lines = [l.split() for l in out.strip().splitlines()]
+    for i in range(5):
+        _, res, steps, x, y, z, dist, td = lines[i]
+        assert int(res) == g["result"][i] and int(steps) == g["steps"][i]
+        np.testing.assert_allclose([float(x), float(y), float(z)], g["hit_position"][i], rtol=RTOL, atol=1e-9)
+        np.testing.assert_allclose([float(dist), float(td)], [g["distance"][i], g["time_dilation"][i]], rtol=RTOL)
+    assert lines[5][0] == "frame" and sum(int(v) for v in lines[5][1:]) == 64 * 36
