@@ -166,12 +166,27 @@ def main():
             "traffic": traffic_from_profile(args.config),
         },
     }
+    if world == 1:
+        out["host_path"] = host_path_rate(c, bh, dk, cfg, cam)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["max_rel_dhit"], out["class_mismatch"] = cpu_baseline(
             args, c, bh, dk, cfg, cam, frame)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_path_rate(c, bh, dk, cfg, cam, frames=3):
+    """bhrt_render_frame into host (pageable numpy) SoA arrays: the PCIe-inclusive rate a C
+    caller of the host API sees. Reported beside `value`, never as it."""
+    lib.render_frame(bh, dk, cfg, cam, c.width, c.height, c.method, c.flags)
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        lib.render_frame(bh, dk, cfg, cam, c.width, c.height, c.method, c.flags)
+    dt = (time.perf_counter() - t0) / frames
+    lib.stats(reset=True)
+    return {"mrays_s": round(c.width * c.height / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 3),
+            "bytes_to_host_per_frame": c.width * c.height * 96}
 
 
 def traffic_from_profile(config):

@@ -20,15 +20,19 @@
 // that many new ray indices from a global queue with ONE atomic and initialises them in
 // the idle lanes (ballot + popcount + lane rank), so a long ray never holds 63 idle lanes.
 //
-// Arithmetic: FP contraction is off by default (BHRT_CONTRACT=0): the kernel then rounds
-// every +,-,* like the reference's x86-64 build, and the only differences left are the
-// last-ulp differences between OCML and glibc sin/cos/acos/atan2/pow.
+// Arithmetic: FP contraction on by default (BHRT_CONTRACT=1; 0 rounds
+// every +,-,* like the reference's x86-64 build); exact divisions without the generic fdiv
+// scaffolding; sincos specialised for the loop's argument range (BHRT_FAST_SINCOS=1, 0 uses
+// OCML) and shifted by angle addition between RK stages.
 #include <hip/hip_runtime.h>
 
 #include "bhrt_kernel.h"
 
 #ifndef BHRT_CONTRACT
 #define BHRT_CONTRACT 1
+#endif
+#ifndef BHRT_FAST_SINCOS
+#define BHRT_FAST_SINCOS 1
 #endif
 #if BHRT_CONTRACT
 #pragma clang fp contract(fast)
@@ -71,6 +75,22 @@ __device__ __forceinline__ double div6(double a) {
     return __builtin_fma(__builtin_fma(-6.0, q, a), y, q);
 }
 
+// fma(a, b, c) with c a compile-time coefficient, as ONE v_fma_f64 whose addend is an SGPR
+// pair (set up by SALU). Left to itself hipcc copies the coefficient into the destination
+// (v_mov_b64) and uses v_fmac_f64: two VALU instructions per Horner step.
+#ifndef BHRT_ASM_FMA
+#define BHRT_ASM_FMA 1
+#endif
+__device__ __forceinline__ double fmac_k(double a, double b, double c) {
+#if BHRT_ASM_FMA
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+#else
+    return __builtin_fma(a, b, c);
+#endif
+}
+
 // sin and cos of one argument, for the trace loop. OCML's sincos
 // spends ~78 VALU per call on a range reduction valid to 2^30+; every argument here (the
 // radius read as an angle by ray_derivatives, theta, phi) stays far below 2^20, where a
@@ -84,6 +104,10 @@ __device__ __attribute__((noinline)) void sincos_ocml(double x, double* s, doubl
 }
 
 __device__ __forceinline__ void bhrt_sincos(double x, double* so, double* co) {
+#if !BHRT_FAST_SINCOS
+    sincos(x, so, co);  // OCML
+    return;
+#endif
     if (!(fabs(x) < 1048576.0)) {
         sincos_ocml(x, so, co);
         return;
@@ -109,12 +133,11 @@ __device__ __forceinline__ void bhrt_sincos(double x, double* so, double* co) {
                      C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                      C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
     const double z = r * r, w = z * z;
-    const double rs_ = __builtin_fma(z, __builtin_fma(z, S4, S3), S2) +
-                       z * w * __builtin_fma(z, S6, S5);
+    const double rs_ = fmac_k(z, fmac_k(z, S4, S3), S2) + z * w * fmac_k(z, S6, S5);
     const double v = z * r;
     const double s = r - ((z * (0.5 * y - v * rs_) - y) - v * S1);
-    const double rc = z * __builtin_fma(z, __builtin_fma(z, C3, C2), C1) +
-                      w * w * __builtin_fma(z, __builtin_fma(z, C6, C5), C4);
+    const double rc = z * fmac_k(z, fmac_k(z, C3, C2), C1) +
+                      w * w * fmac_k(z, fmac_k(z, C6, C5), C4);
     const double hz = 0.5 * z, ww = 1.0 - hz;
     const double c = ww + (((1.0 - ww) - hz) + (z * rc - r * y));
     const int q = (int)n;
@@ -143,11 +166,10 @@ __device__ __forceinline__ bool sincos_shift(double a, double s0, double c0, dou
                      C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                      C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
     const double z = delta * delta, w = z * z;
-    const double r = __builtin_fma(z, __builtin_fma(z, S4, S3), S2) +
-                     z * w * __builtin_fma(z, S6, S5);
-    const double sd = delta + (z * delta) * (S1 + z * r);           // k_sin, tail 0
-    const double rc = z * __builtin_fma(z, __builtin_fma(z, C3, C2), C1) +
-                      w * w * __builtin_fma(z, __builtin_fma(z, C6, C5), C4);
+    const double r = fmac_k(z, fmac_k(z, S4, S3), S2) + z * w * fmac_k(z, S6, S5);
+    const double sd = delta + (z * delta) * fmac_k(z, r, S1);       // k_sin, tail 0
+    const double rc = z * fmac_k(z, fmac_k(z, C3, C2), C1) +
+                      w * w * fmac_k(z, fmac_k(z, C6, C5), C4);
     const double cm1 = z * rc - 0.5 * z;                             // k_cos - 1
     s = s0 + (s0 * cm1 + c0 * sd);
     c = c0 + (c0 * cm1 - s0 * sd);
