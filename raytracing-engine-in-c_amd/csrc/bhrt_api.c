@@ -212,6 +212,29 @@ int bhrt_get_stats(bhrt_stats* out, int reset) {
 /* ======================================================================================= */
 /* launch plumbing                                                                          */
 /* ======================================================================================= */
+/* The disk test's inner <= sqrt(qx^2+qy^2) <= outer (raytracer.c:190-191) without the square
+ * root: sqrt is correctly rounded and monotone, so {s : RN(sqrt(s)) >= inner} = {s >= lo} and
+ * {s : RN(sqrt(s)) <= outer} = {s <= hi} for the thresholds found here by stepping from the
+ * rounded square (a few ulps). NaN bounds keep the comparisons false, as in the reference. */
+static double sqrt_lower_bound(double inner) {
+    if (isnan(inner)) return NAN;
+    if (inner <= 0.0) return -INFINITY;
+    double s = inner * inner;
+    while (s > 0.0 && sqrt(nextafter(s, 0.0)) >= inner) s = nextafter(s, 0.0);
+    while (sqrt(s) < inner) s = nextafter(s, INFINITY);
+    return s;
+}
+
+static double sqrt_upper_bound(double outer) {
+    if (isnan(outer)) return NAN;
+    if (outer < 0.0) return -INFINITY;
+    if (isinf(outer)) return INFINITY;
+    double s = outer * outer;
+    while (sqrt(s) > outer) s = nextafter(s, 0.0);
+    while (!isinf(s) && sqrt(nextafter(s, INFINITY)) <= outer) s = nextafter(s, INFINITY);
+    return s;
+}
+
 static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const AccretionDiskParams* dk,
                       const SimulationConfig* cfg, IntegrationMethod method, int flags) {
     memset(kp, 0, sizeof *kp);
@@ -242,6 +265,8 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
         s->disk_in = dk->inner_radius;
         s->disk_out = dk->outer_radius;
         s->disk_tscale = dk->temperature_scale;
+        s->disk_in_sq = sqrt_lower_bound(dk->inner_radius);
+        s->disk_out_sq = sqrt_upper_bound(dk->outer_radius);
     }
     kp->refill = g_refill;
     kp->cam.rows.row_block = 1;

@@ -29,6 +29,7 @@ typedef struct {
     double h_2_5, h_5, h_15, h_far;
     double max_dist, tol;
     double disk_in, disk_out, disk_tscale;
+    double disk_in_sq, disk_out_sq; /* exact s-bounds of inner <= RN(sqrt(s)) <= outer */
     int max_steps;
     int method;  /* IntegrationMethod */
     int has_disk;

@@ -484,17 +484,23 @@ __device__ __forceinline__ void ray_init_camera(Ray_& R, const bhrt_camera_k& cm
     R.k = 0;
 }
 
-// check_disk_intersection (raytracer.c:159-196), plane "normal" = previous path point
+// check_disk_intersection (raytracer.c:159-196), plane "normal" = previous path point.
+// Two exact shortcuts: t = num/den < 0 when the signs differ (and the quotient cannot
+// underflow), so the division is only formed for t >= 0; and the radial test compares s = qx^2 + qy^2 against
+// the host's thresholds instead of taking sqrt(s) (bhrt_api.c sqrt_lower/upper_bound).
 __device__ __forceinline__ bool disk_test(Ray_& R, double nx, double ny, double nz,
                                           const Scene& sc) {
     const double den = (R.dx * nx + R.dy * ny) + R.dz * nz;
     if (fabs(den) < kEps) return false;
     const double num = -((R.px * nx + R.py * ny) + R.pz * nz);
-    const double t = fabs(den) < 1.0e150 ? div_nr(num, den, rcp_nr(den)) : num / den;
-    if (t < 0.0) return false;
+    const bool normal = fabs(den) < 1.0e150;
+    // t < 0 (|t| > 1e-300, so the quotient cannot underflow to -0, for which t < 0 is false)
+    if (normal && fabs(num) > 1.0e-150 && ((num < 0.0) != (den < 0.0))) return false;
+    const double t = normal ? div_nr(num, den, rcp_nr(den)) : num / den;
+    if (t < 0.0) return false;  // NaN num
     const double qx = R.px + R.dx * t, qy = R.py + R.dy * t, qz = R.pz + R.dz * t;
-    const double rxy = sqrt(qx * qx + qy * qy);
-    if (rxy >= sc.disk_in && rxy <= sc.disk_out) {
+    const double s = qx * qx + qy * qy;
+    if (s >= sc.disk_in_sq && s <= sc.disk_out_sq) {
         R.qx = qx;
         R.qy = qy;
         R.qz = qz;
@@ -509,9 +515,13 @@ enum Term : int { T_NONE = 0, T_HORIZON, T_DISK, T_MAXDIST, T_MAXSTEPS };
 // on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
 template <int METHOD, bool DISK, bool SPIN0, bool FAR>
 __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n) {
+    // :543-548. One test of the sum (non-finite if any component is, or on overflow);
+    // the per-component repair runs only then.
+    if (!isfinite(((R.y[0] + R.y[1]) + (R.y[2] + R.y[3])) + (R.y[4] + R.y[5]))) {
 #pragma unroll
-    for (int i = 0; i < 6; i++)  // :543-548
-        if (!isfinite(R.y[i])) R.y[i] = (i < 4) ? 1.0 : 0.0;
+        for (int i = 0; i < 6; i++)
+            if (!isfinite(R.y[i])) R.y[i] = (i < 4) ? 1.0 : 0.0;
+    }
     // step schedule (:556-571), written as selects so the first true test wins
     const double r = R.y[1];
     double h = sc.h_far;
