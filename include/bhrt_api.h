@@ -192,6 +192,7 @@ typedef struct {
     uint64_t stages_kerr;   /* ... spin != 0 branch                                      */
     uint64_t launches;      /* trace-kernel launches timed                               */
     double   kernel_ms;     /* sum of HIP-event durations of those launches              */
+    uint64_t rays_redone;   /* rays re-traced on the large-argument sincos path          */
 } bhrt_stats;
 
 /* Number of rows of an image of `height` rows owned by shard rows->shard. */

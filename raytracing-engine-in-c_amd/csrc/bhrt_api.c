@@ -193,6 +193,7 @@ static int harvest(devctx_t* c) {
         g_stats.stages_full += w[3];
         g_stats.stages_far += w[4];
         g_stats.stages_kerr += w[5];
+        g_stats.rays_redone += w[6];
         g_stats.launches += 1;
         g_stats.kernel_ms += ms;
     }
@@ -331,6 +332,8 @@ static void fill_camera(bhrt_kparams* kp, const bhrt_camera* cam, int W, int H) 
 static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     if (kp->n <= 0) return 0;
     if (!stream) stream = c->stream;
+    /* the redo list follows the initial-state table (one extra field of the allocation) */
+    kp->redo = (int*)(kp->init + (size_t)BHRT_INIT_FIELDS * (size_t)kp->n);
     if (c->npend == BHRT_RING && harvest(c) != 0) return -1;
     int slot = c->next_slot;
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
@@ -396,7 +399,7 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
         return -1;
     }
     if (ensure(&c->d_init, &c->cap_init,
-               (size_t)BHRT_INIT_FIELDS * sizeof(double) * (size_t)nrows * (size_t)W, 0))
+               (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) * (size_t)nrows * (size_t)W, 0))
         return -1;
     bhrt_kparams kp;
     fill_scene(&kp, bh, dk, cfg, method, flags);
@@ -422,7 +425,8 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
     }
     devctx_t* c = ctx_get(current_device());
     if (!c) return -1;
-    if (ensure(&c->d_init, &c->cap_init, (size_t)BHRT_INIT_FIELDS * sizeof(double) * (size_t)n, 0))
+    if (ensure(&c->d_init, &c->cap_init,
+               (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) * (size_t)n, 0))
         return -1;
     bhrt_kparams kp;
     fill_scene(&kp, bh, dk, cfg, method, flags);

@@ -20,7 +20,8 @@ extern "C" {
 
 enum { BHRT_SRC_RAYS = 0, BHRT_SRC_CAMERA = 1 };
 enum { BHRT_NUM_COUNTERS = 5 }; /* rays, iterations, stages full/far/kerr */
-enum { BHRT_INIT_FIELDS = 15 }; /* y0..y5, y6, y7, dx, dy, dz, px, py, pz, far_ok */
+enum { BHRT_INIT_FIELDS = 21 }; /* y0..y5, y6, y7, dx, dy, dz, px, py, pz, far_ok,
+                                   sin/cos of y1, y2, y3 */
 
 typedef struct {
     /* scene constants (raytracer.c:65-130, 465, 556-571, 652-659; spacetime.c:22) */
@@ -59,10 +60,12 @@ typedef struct {
     int n;                /* rays in this launch                              */
     int refill;           /* refill a wave once >= refill lanes are idle      */
     const Ray* rays;      /* BHRT_SRC_RAYS: device AoS input                  */
-    double* init;         /* BHRT_SRC_RAYS: [BHRT_INIT_FIELDS][n] initial state */
+    double* init;         /* [BHRT_INIT_FIELDS][n] initial state (k_init)      */
+    int* redo;            /* [n] ids of rays re-traced with the large-argument path */
     bhrt_camera_k cam;    /* BHRT_SRC_CAMERA                                  */
     bhrt_frame_soa out;   /* device SoA outputs; NULL fields skipped          */
-    unsigned long long* ctl; /* [0] queue head, [1..5] counters; zeroed per launch */
+    unsigned long long* ctl; /* [0] queue head, [1..5] counters, [6] redo count,
+                                [7] redo queue head; zeroed per launch */
 } bhrt_kparams;
 
 /* launch helpers implemented in geodesic.hip; return 0 or a hipError_t value.

@@ -49,6 +49,7 @@ using Scene = bhrt_scene_k;
 
 struct Counters {
     unsigned rays = 0, iters = 0, full = 0, far_ = 0, kerr = 0;
+    bool huge = false;  // a sincos argument needed the large-argument path (see bhrt_sincos)
 };
 
 // IEEE-exact division without the generic fdiv scaffolding.
@@ -99,18 +100,31 @@ __device__ __forceinline__ double fmac_k(double a, double b, double c) {
 // arguments against glibc (the reference's libm): max 1 ulp, 97% bit-identical.
 // |x| >= 2^20, Inf and NaN take OCML's sincos (not inlined: its Payne-Hanek path must not
 // cost registers in the loop).
-__device__ __attribute__((noinline)) void sincos_ocml(double x, double* s, double* c) {
+#ifndef BHRT_OCML_ATTR
+#define BHRT_OCML_ATTR __attribute__((noinline))
+#endif
+__device__ BHRT_OCML_ATTR void sincos_ocml(double x, double* s, double* c) {
     sincos(x, s, c);
 }
 
-__device__ __forceinline__ void bhrt_sincos(double x, double* so, double* co) {
+// hc == nullptr: |x| >= 2^20 takes OCML's out-of-line path. Otherwise (the hot trace loop,
+// which must contain no call: the call ABI would spill the ray state to scratch) a finite
+// |x| >= 2^20 only raises hc->huge and the ray is re-traced by the HUGE instantiation;
+// Inf and NaN need no special path (the reduction below turns them into NaN, as glibc does).
+__device__ __forceinline__ void bhrt_sincos(double x, double* so, double* co,
+                                            Counters* hc = nullptr) {
 #if !BHRT_FAST_SINCOS
-    sincos(x, so, co);  // OCML
-    return;
+    if (!hc) {
+        sincos(x, so, co);  // OCML
+        return;
+    }
 #endif
     if (!(fabs(x) < 1048576.0)) {
-        sincos_ocml(x, so, co);
-        return;
+        if (!hc) {
+            sincos_ocml(x, so, co);
+            return;
+        }
+        if (fabs(x) <= 1.79769313486231570815e+308) hc->huge = true;
     }
     constexpr double kTwoOverPi = 6.36619772367581382433e-01;
     constexpr double P1 = 1.57079632679489655800e+00;   // pi/2 in three parts
@@ -178,12 +192,17 @@ __device__ __forceinline__ bool sincos_shift(double a, double s0, double c0, dou
 
 // ray_derivatives (raytracer.c:44-154). y = (t, r, theta, phi, tdot, rdot) of the caller,
 // read -- as the reference does -- as (r, theta, phi, v_r, v_theta, v_phi).
-// Trig of theta (= y[1]) for one RK stage: stage 1 evaluates it, later stages shift it.
+// Trig of theta (= y[1]) for one RK stage: stage 1 evaluates it (or, with BHRT_TRIG_CHAIN,
+// takes it from the previous iteration), later stages shift it.
+#ifndef BHRT_TRIG_CHAIN
+#define BHRT_TRIG_CHAIN 1
+#endif
 struct Trig1 {
     double a = __builtin_nan(""), s = 0.0, c = 0.0;  // theta of stage 1 and its sin, cos;
 };                                                   // NaN until stage 1 evaluated them
 
-template <bool SPIN0, bool FAR>
+// HUGE: keep the large-argument sincos path (else flag it, see bhrt_sincos)
+template <bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const Scene& sc,
                                     bool far_ok, Counters& n, Trig1& tr, bool first) {
     d[0] = y[3];
@@ -201,12 +220,17 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         double rsq = r * r;
         double st, ct;
         if (first) {
-            bhrt_sincos(y[1], &st, &ct);
+#if BHRT_TRIG_CHAIN
+            st = tr.s;  // carried from the previous iteration (ray_iterate)
+            ct = tr.c;
+#else
+            bhrt_sincos(y[1], &st, &ct, HUGE ? nullptr : &n);
             tr.a = y[1];
             tr.s = st;
             tr.c = ct;
+#endif
         } else if (!sincos_shift(tr.a, tr.s, tr.c, y[1], st, ct)) {
-            bhrt_sincos(y[1], &st, &ct);
+            bhrt_sincos(y[1], &st, &ct, HUGE ? nullptr : &n);
         }
         double st2 = st * st;
         if (r <= sc.rs_x1_5) {
@@ -260,39 +284,38 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
 
 // rk4_integrate (math_util.c:162-207) on the six live components; the running sum
 // ((k1 + 2k2) + 2k3) + k4 is the reference's left-to-right evaluation order.
-template <bool SPIN0, bool FAR>
+template <bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& sc, bool far_ok,
-                                         Counters& n) {
+                                         Counters& n, Trig1& tr) {
     double k[6], acc[6], yt[6];
     const double hh = 0.5 * h;
-    Trig1 tr;
-    rhs<SPIN0, FAR>(y, k, sc, far_ok, n, tr, true);
+    rhs<SPIN0, FAR, HUGE>(y, k, sc, far_ok, n, tr, true);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         acc[i] = k[i];
         yt[i] = y[i] + hh * k[i];
     }
-    rhs<SPIN0, FAR>(yt, k, sc, far_ok, n, tr, false);
+    rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         acc[i] = acc[i] + 2.0 * k[i];
         yt[i] = y[i] + hh * k[i];
     }
-    rhs<SPIN0, FAR>(yt, k, sc, far_ok, n, tr, false);
+    rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         acc[i] = acc[i] + 2.0 * k[i];
         yt[i] = y[i] + h * k[i];
     }
-    rhs<SPIN0, FAR>(yt, k, sc, far_ok, n, tr, false);
+    rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) y[i] += div6(h * (acc[i] + k[i]));
 }
 
 // rkf45_integrate (math_util.c:212-457), n = 6. Returns true on accept (y <- y5).
-template <bool SPIN0, bool FAR>
+template <bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Scene& sc,
-                                              bool far_ok, Counters& n) {
+                                              bool far_ok, Counters& n, Trig1& tr) {
     constexpr double b21 = 1.0 / 4.0;
     constexpr double b31 = 3.0 / 32.0, b32 = 9.0 / 32.0;
     constexpr double b41 = 1932.0 / 2197.0, b42 = -7200.0 / 2197.0, b43 = 7296.0 / 2197.0;
@@ -305,8 +328,7 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
     constexpr double d1 = 16.0 / 135.0, d3 = 6656.0 / 12825.0, d4 = 28561.0 / 56430.0,
                      d5 = -9.0 / 50.0, d6 = 2.0 / 55.0;
     double k1[6], k2[6], k3[6], k4[6], k5[6], k6[6], yt[6];
-    Trig1 tr;
-    rhs<SPIN0, FAR>(y, k1, sc, far_ok, n, tr, true);
+    rhs<SPIN0, FAR, HUGE>(y, k1, sc, far_ok, n, tr, true);
     bool bad = false;
 #pragma unroll
     for (int i = 0; i < 6; i++) bad |= !isfinite(k1[i]);  // :318-333
@@ -314,21 +336,21 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
     const double hb21 = h * b21;
 #pragma unroll
     for (int i = 0; i < 6; i++) yt[i] = y[i] + hb21 * k1[i];
-    rhs<SPIN0, FAR>(yt, k2, sc, far_ok, n, tr, false);
+    rhs<SPIN0, FAR, HUGE>(yt, k2, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) yt[i] = y[i] + h * (b31 * k1[i] + b32 * k2[i]);
-    rhs<SPIN0, FAR>(yt, k3, sc, far_ok, n, tr, false);
+    rhs<SPIN0, FAR, HUGE>(yt, k3, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) yt[i] = y[i] + h * (b41 * k1[i] + b42 * k2[i] + b43 * k3[i]);
-    rhs<SPIN0, FAR>(yt, k4, sc, far_ok, n, tr, false);
+    rhs<SPIN0, FAR, HUGE>(yt, k4, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++)
         yt[i] = y[i] + h * (b51 * k1[i] + b52 * k2[i] + b53 * k3[i] + b54 * k4[i]);
-    rhs<SPIN0, FAR>(yt, k5, sc, far_ok, n, tr, false);
+    rhs<SPIN0, FAR, HUGE>(yt, k5, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++)
         yt[i] = y[i] + h * (b61 * k1[i] + b62 * k2[i] + b63 * k3[i] + b64 * k4[i] + b65 * k5[i]);
-    rhs<SPIN0, FAR>(yt, k6, sc, far_ok, n, tr, false);
+    rhs<SPIN0, FAR, HUGE>(yt, k6, sc, far_ok, n, tr, false);
     double y5[6];
     double max_error = 0.0;
 #pragma unroll
@@ -349,13 +371,34 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
 
 // spherical_to_cartesian (spacetime.c:229-237)
 __device__ __forceinline__ void sph2cart(double r, double th, double ph, double& x, double& y,
-                                         double& z) {
+                                         double& z, Counters* hc) {
     double st, ct, sp, cp;
-    bhrt_sincos(th, &st, &ct);
-    bhrt_sincos(ph, &sp, &cp);
+    bhrt_sincos(th, &st, &ct, hc);
+    bhrt_sincos(ph, &sp, &cp, hc);
     x = r * st * cp;
     y = r * st * sp;
     z = r * ct;
+}
+
+__device__ __forceinline__ void sph2cart_t(double r, double st, double ct, double sp, double cp,
+                                           double& x, double& y, double& z) {
+    x = r * st * cp;
+    y = r * st * sp;
+    z = r * ct;
+}
+
+// sin, cos of x from those of a, the same component one iteration earlier:
+// exact shift when sincos_shift's preconditions hold, direct evaluation otherwise. Per ray
+// only (never dependent on which wave runs the ray), so results stay reproducible.
+__device__ __forceinline__ void trig_advance(double a, double x, double& s, double& c,
+                                             Counters* hc) {
+    double s1, c1;
+    if (sincos_shift(a, s, c, x, s1, c1)) {
+        s = s1;
+        c = c1;
+    } else {
+        bhrt_sincos(x, &s, &c, hc);
+    }
 }
 
 __device__ __forceinline__ double len3(double x, double y, double z) {
@@ -369,9 +412,16 @@ struct Ray_ {
     double px, py, pz;  // current Cartesian position
     double qx, qy, qz;  // disk hit point
     double dist;
+    double s1, c1, s2, c2, s3, c3;  // sin, cos of y[1], y[2], y[3] (BHRT_TRIG_CHAIN)
     int k;              // iterations executed
     bool far_ok;        // use_analytic_approx && impact_parameter > 0
 };
+
+__device__ __forceinline__ void trig_anchor(Ray_& R, Counters* hc = nullptr) {
+    bhrt_sincos(R.y[1], &R.s1, &R.c1, hc);
+    bhrt_sincos(R.y[2], &R.s2, &R.c2, hc);
+    bhrt_sincos(R.y[3], &R.s3, &R.c3, hc);
+}
 
 // Trig-free part of integrate_photon_path's set-up (raytracer.c:355-466): the initial
 // velocities, dt/dlambda from the null condition, E, L, b. s_* are products of the origin's
@@ -513,14 +563,18 @@ enum Term : int { T_NONE = 0, T_HORIZON, T_DISK, T_MAXDIST, T_MAXSTEPS };
 
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
 // on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
-template <int METHOD, bool DISK, bool SPIN0, bool FAR>
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n) {
+    Counters* const hc = HUGE ? nullptr : &n;
     // :543-548. One test of the sum (non-finite if any component is, or on overflow);
     // the per-component repair runs only then.
     if (!isfinite(((R.y[0] + R.y[1]) + (R.y[2] + R.y[3])) + (R.y[4] + R.y[5]))) {
 #pragma unroll
         for (int i = 0; i < 6; i++)
             if (!isfinite(R.y[i])) R.y[i] = (i < 4) ? 1.0 : 0.0;
+#if BHRT_TRIG_CHAIN
+        trig_anchor(R, hc);
+#endif
     }
     // step schedule (:556-571), written as selects so the first true test wins
     const double r = R.y[1];
@@ -531,15 +585,31 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     h = fmin(h, 0.1);
     bool moved = true;
     n.iters++;
+    Trig1 tr;
+#if BHRT_TRIG_CHAIN
+    tr.a = R.y[1];
+    tr.s = R.s1;
+    tr.c = R.c1;
+    const double a2 = R.y[2], a3 = R.y[3];
+#endif
     if (METHOD == INTEGRATOR_RK4) {
-        rk4_step<SPIN0, FAR>(R.y, h, sc, R.far_ok, n);
+        rk4_step<SPIN0, FAR, HUGE>(R.y, h, sc, R.far_ok, n, tr);
     } else if (METHOD == INTEGRATOR_RKF45) {
-        moved = rkf45_attempt<SPIN0, FAR>(R.y, h, sc, R.far_ok, n);
+        moved = rkf45_attempt<SPIN0, FAR, HUGE>(R.y, h, sc, R.far_ok, n, tr);
     } else {
         moved = false;  // LEAPFROG / YOSHIDA: "not implemented", state unchanged (:616-624)
     }
     double x, y, z;
-    sph2cart(R.y[1], R.y[2], R.y[3], x, y, z);
+#if BHRT_TRIG_CHAIN
+    if (moved) {
+        trig_advance(tr.a, R.y[1], R.s1, R.c1, hc);
+        trig_advance(a2, R.y[2], R.s2, R.c2, hc);
+        trig_advance(a3, R.y[3], R.s3, R.c3, hc);
+    }
+    sph2cart_t(R.y[1], R.s2, R.c2, R.s3, R.c3, x, y, z);
+#else
+    sph2cart(R.y[1], R.y[2], R.y[3], x, y, z, hc);
+#endif
     const double ox = R.px, oy = R.py, oz = R.pz;
     R.dist += len3(x - ox, y - oy, z - oz);
     R.px = x;
@@ -617,6 +687,14 @@ __device__ __forceinline__ void load_init(const bhrt_kparams& kp, int i, Ray_& R
     R.py = f[12 * n + i];
     R.pz = f[13 * n + i];
     R.far_ok = f[14 * n + i] != 0.0;
+#if BHRT_TRIG_CHAIN
+    R.s1 = f[15 * n + i];
+    R.c1 = f[16 * n + i];
+    R.s2 = f[17 * n + i];
+    R.c2 = f[18 * n + i];
+    R.s3 = f[19 * n + i];
+    R.c3 = f[20 * n + i];
+#endif
     R.dist = 0.0;
     R.k = 0;
 }
@@ -655,6 +733,13 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
         f[12 * n + i] = R.py;
         f[13 * n + i] = R.pz;
         f[14 * n + i] = R.far_ok ? 1.0 : 0.0;
+        trig_anchor(R);
+        f[15 * n + i] = R.s1;
+        f[16 * n + i] = R.c1;
+        f[17 * n + i] = R.s2;
+        f[18 * n + i] = R.c2;
+        f[19 * n + i] = R.s3;
+        f[20 * n + i] = R.c3;
     }
 }
 
@@ -671,8 +756,15 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 
 // FAR: some ray may take ray_derivatives' weak-field branch (origin beyond 15 rs). A camera
 // frame knows this once for all its rays (shared origin); ray arrays always assume it.
-template <int METHOD, bool DISK, bool SPIN0, bool FAR>
+// HUGE = false: the hot instantiation, rays [0, kp.n) from queue head ctl[0]. A ray that
+// needs a large-argument sincos (bhrt_sincos) is dropped and its id appended to kp.redo
+// (count ctl[6]). HUGE = true: re-traces kp.redo[0, ctl[6]) from queue head ctl[7].
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE>
 __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
+    unsigned long long* const head = HUGE ? kp.ctl + 7 : kp.ctl;
+    const unsigned long long total =
+        HUGE ? *(volatile unsigned long long*)(kp.ctl + 6) : (unsigned long long)kp.n;
+    if (total == 0) return;
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
     Counters n;
@@ -686,13 +778,13 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         if (!exhausted && (64 - n_live >= kp.refill || n_live == 0)) {
             const int need = 64 - n_live;
             unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(kp.ctl, (unsigned long long)need);
+            if (lane == 0) base = atomicAdd(head, (unsigned long long)need);
             base = __shfl(base, 0);
-            exhausted = base + (unsigned long long)need >= (unsigned long long)kp.n;
+            exhausted = base + (unsigned long long)need >= total;
             if (!live) {
                 const unsigned long long id = base + __popcll(~live_mask & below);
-                if (id < (unsigned long long)kp.n) {
-                    rid = (int)id;
+                if (id < total) {
+                    rid = HUGE ? kp.redo[id] : (int)id;
                     load_init(kp, rid, R);
                     n.rays++;
                     live = true;
@@ -709,8 +801,13 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             continue;
         }
         if (live) {
-            const int term = ray_iterate<METHOD, DISK, SPIN0, FAR>(R, kp.sc, n);
-            if (term != T_NONE) {
+            const int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n);
+            if (!HUGE && n.huge) {  // hand the ray to the HUGE instantiation
+                n.huge = false;
+                n.rays--;
+                kp.redo[atomicAdd(kp.ctl + 6, 1ull)] = rid;
+                live = false;
+            } else if (term != T_NONE) {
                 store_hit(kp.out, rid, R, term, kp.sc);
                 live = false;
             }
@@ -808,6 +905,7 @@ __global__ void k_path(const bhrt_kparams kp, double t0, double ox, double oy, d
     Counters n;
     Ray_ R;
     ray_init_general(R, t0, ox, oy, oz, dx, dy, dz, kp.sc);
+    trig_anchor(R);
     int num = num_in;
     if (path && max_positions > 0) {  // :504-507
         path[0].x = R.px;
@@ -819,7 +917,7 @@ __global__ void k_path(const bhrt_kparams kp, double t0, double ox, double oy, d
     if (kp.sc.max_steps > 0) {
         for (;;) {
             const int k_before = R.k;
-            term = ray_iterate<METHOD, false, SPIN0, true>(R, kp.sc, n);
+            term = ray_iterate<METHOD, false, SPIN0, true, true>(R, kp.sc, n);
             // positions of the iterations executed (a fixed-point jump repeats p_k)
             for (int j = k_before; j < R.k && path && num >= 0 && num < max_positions; j++) {
                 path[num].x = R.px;
@@ -854,10 +952,13 @@ int grid_for(const void* fn, int n) {
 
 template <int METHOD, bool DISK, bool SPIN0, bool FAR>
 int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    static int grid_cap = 0;  // resident workgroups for this instantiation
-    if (grid_cap == 0)
-        grid_cap = grid_for(reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR>),
-                            1 << 30);
+    static int grid_cap = 0, grid_huge = 0;  // resident workgroups per instantiation
+    if (grid_cap == 0) {
+        grid_cap = grid_for(
+            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, false>), 1 << 30);
+        grid_huge = grid_for(
+            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, true>), 1 << 30);
+    }
     if (kp.src == BHRT_SRC_CAMERA)
         k_init<BHRT_SRC_CAMERA><<<grid_for(reinterpret_cast<const void*>(&k_init<BHRT_SRC_CAMERA>),
                                            kp.n), 256, 0, st>>>(kp);
@@ -868,7 +969,10 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
     if (blocks > grid_cap) blocks = grid_cap;
     if (blocks < 1) blocks = 1;
     if (ev0) (void)hipEventRecord(ev0, st);
-    k_trace<METHOD, DISK, SPIN0, FAR><<<blocks, 256, 0, st>>>(kp);
+    k_trace<METHOD, DISK, SPIN0, FAR, false><<<blocks, 256, 0, st>>>(kp);
+    // rays evicted by the large-argument check (normally none: every wave exits at once)
+    k_trace<METHOD, DISK, SPIN0, FAR, true><<<blocks < grid_huge ? blocks : grid_huge, 256, 0,
+                                              st>>>(kp);
     if (ev1) (void)hipEventRecord(ev1, st);
     if (kp.out.rgb_r) {
         if (kp.src == BHRT_SRC_CAMERA)

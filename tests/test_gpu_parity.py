@@ -277,3 +277,60 @@ def test_c_caller_drop_in(bhrt_lib, tmp_path):
         np.testing.assert_allclose([float(x), float(y), float(z)], g["hit_position"][i], rtol=RTOL, atol=1e-9)
         np.testing.assert_allclose([float(dist), float(td)], [g["distance"][i], g["time_dilation"][i]], rtol=RTOL)
     assert lines[5][0] == "frame" and sum(int(v) for v in lines[5][1:]) == 64 * 36
+
+
+def _ulp_stable(oracle, rays, bh, disk, cfg):
+    """Rays whose oracle result (class, steps, hit to 1e-9) is unchanged when the origin
+    moves by one ulp either way: the inputs the reference itself treats as well-conditioned."""
+    base = oracle.trace_rays(rays, bh, disk, cfg)
+    keep = np.ones(len(rays), dtype=bool)
+    for direction in (np.inf, -np.inf):
+        moved = rays.copy()
+        moved["origin"] = np.nextafter(rays["origin"], direction)
+        o = oracle.trace_rays(moved, bh, disk, cfg)
+        keep &= (o["result"] == base["result"]) & (o["steps"] == base["steps"])
+        for f in ("hit_x", "hit_y", "hit_z", "distance"):
+            keep &= np.abs(o[f] - base[f]) <= 1e-7 * np.maximum(np.abs(base[f]), 1.0)
+    return keep
+
+
+def test_large_argument_rays_take_the_redo_path(bhrt_lib, oracle):
+    """Rays whose sincos arguments reach |x| >= 2^20 are evicted from the hot trace kernel,
+    which has no large-argument reduction, and re-traced by its HUGE instantiation
+    (geodesic.hip k_trace). Results must equal the oracle's for every ray, whichever kernel
+    finished it.
+
+    Groups of 64: (1) |origin| 25; (2) |origin| 2e6; (3) 0.25 below 2^20, where state[1]
+    (read as theta by ray_derivatives) rises through 2^20 in the first steps (checked with
+    an instrumented oracle) -- with the carried trig (BHRT_TRIG_CHAIN) such rays are
+    reached by exact shifts and need no large-argument evaluation; (4) 1e-8..1e-7 outside
+    the horizon, where dt/dlambda is huge and single RK stages jump state[1] past 2^20, so
+    the shift does not apply and the ray is evicted. No group sits at |origin| = 15 rs (the
+    far-field threshold) and no direction is exactly radial (v_phi would be a cancellation
+    residual that FMA contraction decides, switching the far-field branch through
+    impact_parameter > 0); group (4) keeps only the rays whose oracle result survives a
+    one-ulp move of the origin (_ulp_stable); so does every other group."""
+    rng = np.random.default_rng(7)
+    n = 320
+    rays = np.zeros(n, dtype=abi.RAY_DTYPE)
+    radius = np.concatenate([np.full(64, 25.0), np.full(64, 2.0e6), np.full(64, 2.0**20 - 0.25),
+                             2.0 + 10.0 ** rng.uniform(-8.0, -7.0, 128)])
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1)[:, None]
+    rays["origin"] = u * radius[:, None]
+    d = rng.normal(size=(n, 3))
+    rays["direction"] = d / np.linalg.norm(d, axis=1)[:, None]
+    bh = abi.black_hole(1.0, 0.0)
+    cfg = abi.sim_config(time_step=0.1, max_dist=1.0e8, max_steps=120)
+    dk = abi.disk(6.0, 20.0, 1.0, 1.0)
+    for disk in (None, dk):
+        keep = _ulp_stable(oracle, rays, bh, disk, cfg)
+        sel = rays[keep]
+        assert all(keep[a:b].sum() >= 16 for a, b in ((0, 64), (64, 128), (128, 192), (192, n)))
+        bhrt_lib.stats(reset=True)
+        got = bhrt_lib.trace_rays(sel, bh, disk, cfg)
+        st = bhrt_lib.stats(reset=True)
+        want = oracle.trace_rays(sel, bh, disk, cfg)
+        compare(got, want, RTOL, False, "large-argument rays")
+        assert st["rays"] == len(sel)
+        assert st["rays_redone"] > 0, st
