@@ -6,7 +6,7 @@
 // its quirks: the index-shifted ray_derivatives (raytracer.c:44-154), the clamps, the
 // radius step schedule and the zero-acceleration "Kerr" branch. See DESIGN.md section 2.
 //
-// Restructurings that leave every pinned output unchanged (DESIGN.md section 2.3):
+// Restructurings that leave every pinned output unchanged (DESIGN.md section 2.2):
 //   * trace_ray stores the whole path and scans it for the first disk crossing afterwards
 //     (raytracer.c:698-759); here each segment is tested as soon as it exists and the lane
 //     stops at the first hit.
@@ -23,7 +23,9 @@
 // Arithmetic: FP contraction on by default (BHRT_CONTRACT=1; 0 rounds
 // every +,-,* like the reference's x86-64 build); exact divisions without the generic fdiv
 // scaffolding; sincos specialised for the loop's argument range (BHRT_FAST_SINCOS=1, 0 uses
-// OCML) and shifted by angle addition between RK stages.
+// OCML), shifted by angle addition between RK stages and carried from one iteration to the
+// next (BHRT_TRIG_CHAIN=1). The hot instantiation contains no call: rays that need a
+// large-argument sincos are re-traced by a second launch (k_trace HUGE=true).
 #include <hip/hip_runtime.h>
 
 #include "bhrt_kernel.h"
@@ -52,7 +54,7 @@ struct Counters {
     bool huge = false;  // a sincos argument needed the large-argument path (see bhrt_sincos)
 };
 
-// IEEE-exact division without the generic fdiv scaffolding (DESIGN.md section 4.2).
+// IEEE-exact division without the generic fdiv scaffolding (DESIGN.md §2.3).
 // rcp_nr is the reciprocal refinement the compiler's f64 fdiv performs after v_div_scale
 // (v_rcp_f64 + two Newton steps); div_nr is its quotient step (q = a*y, one FMA residual,
 // one FMA correction). For operands in the normal range v_div_scale is the identity, so
@@ -78,7 +80,7 @@ __device__ __forceinline__ double div6(double a) {
 
 // fma(a, b, c) with c a compile-time coefficient, as ONE v_fma_f64 whose addend is an SGPR
 // pair (set up by SALU). Left to itself hipcc copies the coefficient into the destination
-// (v_mov_b64) and uses v_fmac_f64: two VALU instructions per Horner step (DESIGN.md 4.3).
+// (v_mov_b64) and uses v_fmac_f64: two VALU instructions per Horner step (DESIGN.md §2.3).
 #ifndef BHRT_ASM_FMA
 #define BHRT_ASM_FMA 1
 #endif
@@ -92,7 +94,7 @@ __device__ __forceinline__ double fmac_k(double a, double b, double c) {
 #endif
 }
 
-// sin and cos of one argument, for the trace loop (DESIGN.md section 4.3). OCML's sincos
+// sin and cos of one argument, for the trace loop (DESIGN.md §2.3). OCML's sincos
 // spends ~78 VALU per call on a range reduction valid to 2^30+; every argument here (the
 // radius read as an angle by ray_derivatives, theta, phi) stays far below 2^20, where a
 // three-constant Cody-Waite reduction with FMA is exact up to a double-double tail. The
@@ -161,7 +163,7 @@ __device__ __forceinline__ void bhrt_sincos(double x, double* so, double* co,
     *co = ((q + 1) & 2) ? -cc : cc;
 }
 
-// sin and cos of a + delta from s0 = sin(a), c0 = cos(a) (DESIGN.md section 4.3). Every
+// sin and cos of a + delta from s0 = sin(a), c0 = cos(a) (DESIGN.md §2.3). Every
 // RK4/RKF45 stage after the first evaluates ray_derivatives at theta = y1 + delta with a
 // small delta (the stage increment of state[1]; |delta| < 0.09 on a full C2 frame), so one
 // direct sincos per iteration serves all stages: sin(delta) and cos(delta) - 1 come from
@@ -387,7 +389,7 @@ __device__ __forceinline__ void sph2cart_t(double r, double st, double ct, doubl
     z = r * ct;
 }
 
-// sin, cos of x from those of a, the same component one iteration earlier (DESIGN.md 4.3):
+// sin, cos of x from those of a, the same component one iteration earlier (DESIGN.md §2.3):
 // exact shift when sincos_shift's preconditions hold, direct evaluation otherwise. Per ray
 // only (never dependent on which wave runs the ray), so results stay reproducible.
 __device__ __forceinline__ void trig_advance(double a, double x, double& s, double& c,

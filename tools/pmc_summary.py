@@ -16,11 +16,14 @@ per = collections.defaultdict(list)
 for p in sorted(glob.glob(f"{src}/p*/pass_counter_collection.csv")):
     acc = collections.defaultdict(float)
     for row in csv.DictReader(open(p)):
+        # the hot instantiation only (HUGE = false); the redo launch is normally empty
+        if not row.get("Kernel_Name", "").rstrip().endswith("false>(bhrt_kparams)"):
+            continue
         acc[(row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
     for (disp, name), v in acc.items():
         per[name].append(v)
 avg = {k: sum(v) / len(v) for k, v in per.items()}
-out = {"config": cfg, "kernel": "k_trace", "counters_per_launch": avg}
+out = {"config": cfg, "kernel": "k_trace (hot instantiation, HUGE=false)", "counters_per_launch": avg}
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     out["fetch_bytes_raw"] = avg["FETCH_SIZE"] * 1024
     out["write_bytes"] = avg["WRITE_SIZE"] * 1024
