@@ -77,8 +77,7 @@ def main():
     c = configs.CONFIGS[args.config]
     bh, dk, cfg = c.scene()
     cam = configs.camera(args.camera)
-    W, H1 = c.width, c.height
-    H = H1 * world
+    W, H = c.width, c.bench_height(world)
     rows = abi.Rows(ROW_BLOCK, rank, world)
     n_rows = lib.shard_rows(H, rows)
     n = n_rows * W
@@ -136,7 +135,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": c.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (deterministic camera-B frame, no input data)",
@@ -167,7 +166,7 @@ def main():
         },
     }
     if world == 1:
-        out["host_path"] = host_path_rate(c, bh, dk, cfg, cam)
+        out["host_path"] = host_path_rate(c, bh, dk, cfg, cam, W, H)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["max_rel_dhit"], out["class_mismatch"] = cpu_baseline(
             args, c, bh, dk, cfg, cam, frame)
@@ -176,17 +175,17 @@ def main():
         dist.destroy_process_group()
 
 
-def host_path_rate(c, bh, dk, cfg, cam, frames=3):
+def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=3):
     """bhrt_render_frame into host (pageable numpy) SoA arrays: the PCIe-inclusive rate a C
     caller of the host API sees. Reported beside `value`, never as it."""
-    lib.render_frame(bh, dk, cfg, cam, c.width, c.height, c.method, c.flags)
+    lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
     t0 = time.perf_counter()
     for _ in range(frames):
-        lib.render_frame(bh, dk, cfg, cam, c.width, c.height, c.method, c.flags)
+        lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
     dt = (time.perf_counter() - t0) / frames
     lib.stats(reset=True)
-    return {"mrays_s": round(c.width * c.height / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 3),
-            "bytes_to_host_per_frame": c.width * c.height * 96}
+    return {"mrays_s": round(W * H / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 3),
+            "bytes_to_host_per_frame": W * H * 96}
 
 
 def traffic_from_profile(config):
@@ -209,7 +208,7 @@ def cpu_baseline(args, c, bh, dk, cfg, cam, frame):
     except (FileNotFoundError, OSError):
         checker, kind = orc.oracle(), "port"
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    W, H = c.width, c.height
+    W, H = c.width, c.bench_height(1)
     rows = list(range(0, H, args.cpu_rows_stride))
     got = {f: frame.views[f].view(-1).cpu().numpy().reshape(H, W)[rows] for f in FIELDS}
     t0 = time.perf_counter()

@@ -36,6 +36,14 @@ class Config:
     flags: int
     gpus: int          # GPUs the configuration is quoted on
     note: str
+    scaling: str = "weak"  # bench.py at N GPUs: "weak" = N x gpu_rows rows, "strong" = height
+    gpu_rows: int = 0      # rows per GPU under weak scaling (0: height)
+
+    def bench_height(self, n_gpus):
+        """Image rows bench.py renders on n_gpus GPUs."""
+        if self.scaling == "strong":
+            return self.height
+        return (self.gpu_rows or self.height) * n_gpus
 
     def scene(self):
         bh = abi.black_hole(1.0, self.spin)
@@ -53,7 +61,8 @@ CONFIGS = {
                  "1920x1080 Schwarzschild + disk, RKF45 tol 1e-6, 1 GPU"),
     "C4": Config("C4", 3840, 2160, 0.9, True, abi.INTEGRATOR_RK4, 1e-6, 1000,
                  abi.BHRT_FLAG_DOPPLER, 8,
-                 "3840x2160 Kerr a=0.9 + disk + Doppler/beaming, RK4, 8 GPUs"),
+                 "3840x2160 Kerr a=0.9 + disk + Doppler/beaming, RK4, 8 GPUs", "strong"),
     "C5": Config("C5", 7680, 4320, 0.99, False, abi.INTEGRATOR_RKF45, 1e-8, 2000, 0, 8,
-                 "7680x4320 Kerr a=0.99, RKF45 tol 1e-8, 2000 steps, 8 GPUs weak scaling"),
+                 "7680x4320 Kerr a=0.99, RKF45 tol 1e-8, 2000 steps, 8 GPUs weak scaling: one "
+                 "7680x540 slab per GPU", "weak", 540),
 }
