@@ -97,6 +97,32 @@ SchwarzschildMetric calculate_schwarzschild_metric(double r, const BlackHolePara
 double calculate_time_dilation(double r, const BlackHoleParams* blackhole);/* spacetime.c:192 */
 void cartesian_to_spherical(const Vector3D* cartesian, Vector3D* spherical);/* spacetime.c:201 */
 void spherical_to_cartesian(const Vector3D* spherical, Vector3D* cartesian);/* spacetime.c:229 */
+KerrMetric calculate_kerr_metric(double r, double theta, const BlackHoleParams* blackhole);
+                                                                         /* spacetime.c:38 */
+BlackHoleMetric calculate_metric(double r, double theta, const BlackHoleParams* blackhole);
+                                                                         /* spacetime.c:74 */
+double calculate_effective_potential(double r, double l, const BlackHoleParams* blackhole);
+                                                                         /* spacetime.c:242 */
+double calculate_ergosphere_radius(double theta, const BlackHoleParams* blackhole);
+                                                                         /* spacetime.c:314 */
+int calculate_kerr_metric_bl(const double position[4], double a, double M, KerrMetric* metric);
+                                                                         /* spacetime.c:377 */
+int calculate_inverse_kerr_metric(const double position[4], double a, double M,
+                                  KerrMetric* inv_metric);               /* spacetime.c:429 */
+int calculate_kerr_christoffel(const double position[4], double a, double M,
+                               double christoffel[4][4][4]);             /* spacetime.c:483 */
+double calculate_kerr_isco(double a, double M, bool prograde);           /* spacetime.c:548 */
+double calculate_kerr_event_horizon(double a, double M);                 /* spacetime.c:565 */
+double calculate_kerr_ergosphere(double a, double M, double theta);      /* spacetime.c:577 */
+int calculate_frame_dragging(const double position[4], double a, double M, double velocity[3]);
+                                                                         /* spacetime.c:590 */
+int calculate_kerr_geodesic(const double position[4], const double velocity[4], double a,
+                            double M, double acceleration[4]);           /* spacetime.c:624 */
+void calculate_christoffel_symbols(double r, double theta, const BlackHoleParams* blackhole,
+                                   double christoffel[4][4][4]);         /* spacetime.c:93 */
+void geodesic_equation(const double position[4], const double velocity[4],
+                       const BlackHoleParams* blackhole, double acceleration[4]);
+                                                                         /* spacetime.c:166 */
 
 /* math_util.h */
 Vector3D vector3D_add(const Vector3D a, const Vector3D b);               /* math_util.c:31 */
@@ -112,6 +138,31 @@ int rkf45_integrate(ODEFunction f, double y[], int n, double* t, double h_try, d
                     double eps_rel, void* params);                       /* math_util.c:212 */
 void temperature_to_rgb(double temperature, double rgb[3]);              /* math_util.c:463 */
 double clamp(double value, double min, double max);                      /* math_util.c:505 */
+void leapfrog_integrate(ODEFunctionSecondOrder f, double* x, double* v, int n, double t,
+                        double dt, void* params);                        /* math_util.c:125 */
+
+/* particle_sim.h -- host bookkeeping; update_particles runs on the GPU (one lane per
+ * particle). */
+int particle_system_init(ParticleSystem* system, int initial_capacity);   /* particle_sim.c:73 */
+void particle_system_cleanup(ParticleSystem* system);                    /* particle_sim.c:96 */
+int add_particle(ParticleSystem* system, const Vector3D* position, const Vector3D* velocity,
+                 double mass, ParticleType type);                        /* particle_sim.c:108 */
+int update_particles(ParticleSystem* system, const BlackHoleParams* blackhole,
+                     const SimulationConfig* config);                    /* particle_sim.c:505 */
+/* defined (non-static) by the reference but not declared in its headers */
+Particle* find_particle(ParticleSystem* system, int particle_id);        /* particle_sim.c:138 */
+int remove_particle(ParticleSystem* system, int particle_id);            /* particle_sim.c:155 */
+int calculate_particle_orbit(const ParticleSystem* system, int particle_id,
+                             const BlackHoleParams* blackhole, OrbitalParams* params);
+                                                                         /* particle_sim.c:571 */
+int calculate_circular_orbit(double r, const BlackHoleParams* blackhole, Vector3D* velocity);
+                                                                         /* particle_sim.c:604 */
+int create_accretion_disk(ParticleSystem* system, const BlackHoleParams* blackhole,
+                          const AccretionDiskParams* disk, int num_particles);
+                                                                         /* particle_sim.c:339 */
+int generate_hawking_radiation(ParticleSystem* system, const BlackHoleParams* blackhole,
+                               int num_particles, const SimulationConfig* config);
+                                                                         /* particle_sim.c:427 */
 
 /* --- context API (include/blackhole_api.h:47-255, src/blackhole_api.c) --- */
 BHContextHandle bh_initialize(void);                                     /* blackhole_api.c:52 */
@@ -131,6 +182,18 @@ BHErrorCode bh_trace_ray(BHContextHandle context, const double origin[3],
                          const double direction[3], RayTraceHit* hit);   /* blackhole_api.c:182 */
 BHErrorCode bh_trace_rays_batch(BHContextHandle context, const Ray* rays, RayTraceHit* hits,
                                 int count);                              /* blackhole_api.c:225 */
+void* bh_create_particle_system(BHContextHandle context, int capacity); /* blackhole_api.c:256 */
+void bh_destroy_particle_system(BHContextHandle context, void* system);  /* blackhole_api.c:280 */
+int bh_add_test_particle(BHContextHandle context, void* system, const double position[3],
+                         const double velocity[3], double mass);         /* blackhole_api.c:296 */
+int bh_create_accretion_disk_particles(BHContextHandle context, void* system,
+                                       int num_particles);               /* blackhole_api.c:318 */
+int bh_generate_hawking_radiation(BHContextHandle context, void* system, int num_particles);
+                                                                         /* blackhole_api.c:343 */
+BHErrorCode bh_update_particles(BHContextHandle context, void* system);  /* blackhole_api.c:364 */
+BHErrorCode bh_get_particle_data(BHContextHandle context, void* system, double* positions,
+                                 double* velocities, int* types, int* count);
+                                                                         /* blackhole_api.c:384 */
 BHErrorCode bh_calculate_time_dilation(BHContextHandle context, const double position1[3],
                                        const double position2[3], double* time_ratio);
                                                                          /* blackhole_api.c:432 */
@@ -236,6 +299,13 @@ int bhrt_device_count(void);
 /* Tuning knob: refill a wavefront's finished lanes once at least this many are idle
  * (1..64, default 8). Affects speed only. */
 void bhrt_set_refill_threshold(int lanes);
+
+/* update_particles (particle_sim.c:505-566) applied `steps` times in one device round trip:
+ * the particle array is copied to the GPU once, stepped `steps` times by the HIP kernel and
+ * copied back (steps == 1 is exactly update_particles). Returns 0, or -1 on invalid
+ * arguments / HIP failure. If kernel_ms is not NULL it receives the kernels' HIP-event time. */
+int bhrt_update_particles_steps(ParticleSystem* system, const BlackHoleParams* blackhole,
+                                const SimulationConfig* config, int steps, double* kernel_ms);
 
 /* Last error message of the calling thread ("" if none). */
 const char* bhrt_last_error(void);

@@ -20,6 +20,7 @@
 #ifndef BHRT_TYPES_H
 #define BHRT_TYPES_H
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -35,6 +36,21 @@ typedef struct { double t, x, y, z; } Vector4D;
 typedef struct { Vector3D origin; Vector3D direction; } Ray;
 
 typedef struct { double g_tt, g_rr, g_thth, g_phph; } SchwarzschildMetric;
+
+/* include/blackhole_types.h:53-72 (Kerr helpers of spacetime.c) */
+typedef struct {
+    double g_tt, g_tphi, g_rr, g_thth;
+    double g_thetatheta;         /* set by calculate_kerr_metric_bl only                    */
+    double g_phiphi, g_phit;
+} KerrMetric;
+
+typedef struct {
+    int is_kerr;
+    union {
+        SchwarzschildMetric schwarzschild;
+        KerrMetric kerr;
+    } metric;
+} BlackHoleMetric;
 
 /* ---- physical scene ---------------------------------------------------------------------- */
 typedef struct {
@@ -131,8 +147,54 @@ typedef struct {
     double observer_distance, fov;
 } GPUShaderParams;
 
-/* ODE right-hand side used by the generic host integrators (math_util.h:160) */
+/* ODE right-hand sides used by the generic host integrators (math_util.h:163, 173) */
 typedef void (*ODEFunction)(double t, const double y[], double dydt[], void* params);
+typedef void (*ODEFunctionSecondOrder)(double t, const double x[], const double v[], double a[],
+                                       void* params);
+
+/* ---- particle simulation (include/particle_sim.h:15-75) ---------------------------------- */
+typedef enum {
+    PARTICLE_TEST,
+    PARTICLE_DISK,
+    PARTICLE_HAWKING,
+    PARTICLE_JET
+} ParticleType;
+
+typedef struct {
+    Vector3D position;
+    Vector3D velocity;
+    Vector3D acceleration;       /* never written by the reference                          */
+    double mass;
+    double energy;               /* never written by the reference                          */
+    double angular_momentum;     /* never written by the reference                          */
+    double proper_time;          /* never written by the reference                          */
+    double coordinate_time;      /* never written by the reference                          */
+    ParticleType type;
+    int active;
+    int id;
+    double age;
+    double temperature;
+    double time_dilation;        /* written by the geodesic update only                     */
+} Particle;
+
+typedef struct {
+    double semi_major_axis;
+    double eccentricity;
+    double inclination;
+    double longitude_of_ascending_node;
+    double argument_of_periapsis;
+    double mean_anomaly;
+    double specific_angular_momentum;
+    double specific_energy;
+} OrbitalParams;
+
+typedef struct {
+    Particle* particles;
+    int capacity;
+    int count;
+    int next_id;
+    BlackHoleParams* blackhole;  /* never set by the reference                               */
+} ParticleSystem;
 
 /* ---- layout pins (x86-64 SysV) --------------------------------------------- */
 #if defined(__cplusplus)
@@ -156,6 +218,14 @@ BHRT_STATIC_ASSERT(offsetof(RayTraceHit, sky_direction) == 80, "RayTraceHit.sky_
 BHRT_STATIC_ASSERT(offsetof(RayTraceHit, color) == 120, "RayTraceHit.color");
 BHRT_STATIC_ASSERT(offsetof(RayTraceHit, optical_depth) == 152, "RayTraceHit.optical_depth");
 BHRT_STATIC_ASSERT(sizeof(RayTraceResult) == 4, "enum size");
+BHRT_STATIC_ASSERT(sizeof(KerrMetric) == 56, "KerrMetric");
+BHRT_STATIC_ASSERT(sizeof(BlackHoleMetric) == 64, "BlackHoleMetric");
+BHRT_STATIC_ASSERT(sizeof(Particle) == 152, "Particle");
+BHRT_STATIC_ASSERT(offsetof(Particle, type) == 112, "Particle.type");
+BHRT_STATIC_ASSERT(offsetof(Particle, age) == 128, "Particle.age");
+BHRT_STATIC_ASSERT(offsetof(Particle, time_dilation) == 144, "Particle.time_dilation");
+BHRT_STATIC_ASSERT(sizeof(ParticleSystem) == 32, "ParticleSystem");
+BHRT_STATIC_ASSERT(sizeof(OrbitalParams) == 64, "OrbitalParams");
 
 #ifdef __cplusplus
 }

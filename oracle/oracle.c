@@ -448,6 +448,90 @@ void orc_camera_ray_direction(int px, int py, double ox, double oy, int W, int H
 }
 
 /* ---- drivers ---- */
+/* ---- particle_sim.c: update_particles and its two steppers ---- */
+static void christoffel(double r, double theta, const BlackHoleParams* bh, double G[4][4][4]) {
+    /* spacetime.c:93-161 */
+    memset(G, 0, 4 * 4 * 4 * sizeof(double));
+    if (bh->spin == 0.0) {
+        double rs = bh->schwarzschild_radius;
+        if (r <= rs + BH_EPSILON) r = rs + BH_EPSILON;
+        double sin_theta = sin(theta), cos_theta = cos(theta);
+        G[0][0][1] = G[0][1][0] = rs / (2.0 * r * (r - rs));
+        G[1][0][0] = rs * (r - rs) / (2.0 * r * r * r);
+        G[1][1][1] = -rs / (2.0 * r * (r - rs));
+        G[1][2][2] = -(r - rs);
+        G[1][3][3] = -(r - rs) * sin_theta * sin_theta;
+        G[2][1][2] = G[2][2][1] = 1.0 / r;
+        G[2][3][3] = -sin_theta * cos_theta;
+        G[3][1][3] = G[3][3][1] = 1.0 / r;
+        G[3][2][3] = G[3][3][2] = cos_theta / sin_theta;
+    } else {
+        double M = bh->mass, a = bh->spin * M;
+        if (r <= bh->r_plus + BH_EPSILON) r = bh->r_plus + BH_EPSILON;
+        double sin_theta = sin(theta), cos_theta = cos(theta);
+        double sin_theta_sq = sin_theta * sin_theta, cos_theta_sq = cos_theta * cos_theta;
+        double Sigma = r * r + a * a * cos_theta_sq;
+        double Sigma_sq = Sigma * Sigma;
+        G[0][0][1] = M * (r * r - a * a * cos_theta_sq) / Sigma_sq;
+        G[0][1][0] = G[0][0][1];
+        G[0][1][3] = -a * M * sin_theta_sq * (r * r - a * a * cos_theta_sq) / Sigma_sq;
+        G[0][3][1] = G[0][1][3];
+    }
+}
+
+static void particle_geodesic(Particle* p, const BlackHoleParams* bh, const SimulationConfig* cfg) {
+    /* particle_sim.c:232-304 (particle_derivatives :33-68, geodesic_equation spacetime.c:166-187) */
+    Vector3D sph;
+    cart2sph(&p->position, &sph);
+    double r = sph.x, theta = sph.y, phi = sph.z;
+    double state[8] = {0.0, r, theta, phi, 1.0, 0.0, 0.0, 0.0};
+    double v_mag = v_len(p->velocity);
+    state[5] = v_mag * cos(theta) * cos(phi);
+    state[6] = v_mag * sin(phi);
+    state[7] = v_mag * sin(theta) * cos(phi);
+    double G[4][4][4], acc[4] = {0.0, 0.0, 0.0, 0.0};
+    christoffel(state[1], state[2], bh, G);
+    for (int mu = 0; mu < 4; mu++)
+        for (int al = 0; al < 4; al++)
+            for (int be = 0; be < 4; be++) acc[mu] -= G[mu][al][be] * state[4 + al] * state[4 + be];
+    double d[8] = {state[4], state[5], state[6], state[7], acc[0], acc[1], acc[2], acc[3]};
+    for (int i = 0; i < 8; i++) state[i] += d[i] * cfg->time_step;
+    Vector3D ns = {state[1], state[2], state[3]};
+    sph2cart(&ns, &p->position);
+    double v_r = state[5], v_theta = state[6], v_phi = state[7];
+    p->velocity.x = v_r * sin(theta) * cos(phi) + r * v_theta * cos(theta) * cos(phi) - r * sin(theta) * v_phi * sin(phi);
+    p->velocity.y = v_r * sin(theta) * sin(phi) + r * v_theta * cos(theta) * sin(phi) + r * sin(theta) * v_phi * cos(phi);
+    p->velocity.z = v_r * cos(theta) - r * v_theta * sin(theta);
+    p->time_dilation = time_dilation(state[1], bh->schwarzschild_radius);
+}
+
+static void particle_newtonian(Particle* p, const BlackHoleParams* bh, const SimulationConfig* cfg) {
+    /* particle_sim.c:306-337 */
+    double r = v_len(p->position);
+    double accel_mag = bh->mass / (r * r);
+    Vector3D accel_dir = v_scale(p->position, -1.0 / r);
+    Vector3D acceleration = v_scale(accel_dir, accel_mag);
+    p->velocity = v_add(p->velocity, v_scale(acceleration, cfg->time_step));
+    p->position = v_add(p->position, v_scale(p->velocity, cfg->time_step));
+}
+
+void orc_update_particles(Particle* ps, int count, const BlackHoleParams* bh,
+                          const SimulationConfig* cfg, int steps) {
+    for (int s = 0; s < steps; s++) /* particle_sim.c:505-566, once per step */
+        for (int i = 0; i < count; i++) {
+            Particle* p = &ps[i];
+            if (!p->active) continue;
+            p->age += cfg->time_step;
+            double r = v_len(p->position);
+            if (p->type == PARTICLE_TEST && r < 20.0 * bh->schwarzschild_radius)
+                particle_geodesic(p, bh, cfg);
+            else
+                particle_newtonian(p, bh, cfg);
+            r = v_len(p->position);
+            if (r <= bh->schwarzschild_radius) p->active = 0;
+        }
+}
+
 int orc_shard_rows(int H, const bhrt_rows* rows) {
     if (!rows || rows->num_shards <= 1) return H;
     int B = rows->row_block, n = 0;

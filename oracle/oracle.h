@@ -58,6 +58,9 @@ int orc_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
                    const AccretionDiskParams* disk, const SimulationConfig* cfg,
                    IntegrationMethod method, int flags, const bhrt_frame_soa* out, int nthreads);
 /* rows of a shard (same rule as bhrt_shard_rows) and local row j -> image row */
+/* update_particles (particle_sim.c:505-566) applied `steps` times to ps[0, count) */
+void orc_update_particles(Particle* ps, int count, const BlackHoleParams* bh,
+                          const SimulationConfig* cfg, int steps);
 int orc_shard_rows(int H, const bhrt_rows* rows);
 int orc_shard_row(int j, const bhrt_rows* rows);
 

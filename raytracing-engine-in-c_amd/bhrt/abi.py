@@ -112,6 +112,42 @@ HIT_DTYPE = np.dtype({
     "itemsize": 160})
 RAY_DTYPE = np.dtype([("origin", np.float64, 3), ("direction", np.float64, 3)])
 
+# particle_sim.h:15-75 (Particle 152 B, ParticleSystem 32 B; pinned in bhrt_types.h)
+PARTICLE_TEST, PARTICLE_DISK, PARTICLE_HAWKING, PARTICLE_JET = 0, 1, 2, 3
+
+
+class Particle(C.Structure):
+    _fields_ = [("position", Vector3D), ("velocity", Vector3D), ("acceleration", Vector3D),
+                ("mass", C.c_double), ("energy", C.c_double), ("angular_momentum", C.c_double),
+                ("proper_time", C.c_double), ("coordinate_time", C.c_double),
+                ("type", C.c_int), ("active", C.c_int), ("id", C.c_int), ("age", C.c_double),
+                ("temperature", C.c_double), ("time_dilation", C.c_double)]
+
+
+class ParticleSystem(C.Structure):
+    _fields_ = [("particles", C.POINTER(Particle)), ("capacity", C.c_int), ("count", C.c_int),
+                ("next_id", C.c_int), ("blackhole", C.c_void_p)]
+
+
+PARTICLE_DTYPE = np.dtype({
+    "names": ["position", "velocity", "acceleration", "mass", "energy", "angular_momentum",
+              "proper_time", "coordinate_time", "type", "active", "id", "age", "temperature",
+              "time_dilation"],
+    "formats": [(np.float64, 3), (np.float64, 3), (np.float64, 3)] + [np.float64] * 5 +
+               [np.int32] * 3 + [np.float64] * 3,
+    "offsets": [0, 24, 48, 72, 80, 88, 96, 104, 112, 116, 120, 128, 136, 144],
+    "itemsize": 152})
+
+
+def particles_view(ps):
+    """numpy view (no copy) of ps.particles[0:count]."""
+    if ps.count <= 0:
+        return np.zeros(0, dtype=PARTICLE_DTYPE)
+    buf = (C.c_char * (ps.count * 152)).from_address(C.addressof(ps.particles.contents))
+    return np.frombuffer(buf, dtype=PARTICLE_DTYPE)
+
+
+assert C.sizeof(Particle) == 152 and C.sizeof(ParticleSystem) == 32
 assert C.sizeof(RayTraceHit) == 160 and C.sizeof(SimulationConfig) == 72
 assert C.sizeof(BlackHoleParams) == 64 and C.sizeof(AccretionDiskParams) == 48
 

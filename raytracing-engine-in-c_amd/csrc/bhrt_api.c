@@ -23,6 +23,7 @@
 #pragma GCC visibility push(default)
 #include "../../include/bhrt_api.h"
 #pragma GCC visibility pop
+#include "bhrt_host.h"
 #include "bhrt_kernel.h"
 
 /* ======================================================================================= */
@@ -30,13 +31,14 @@
 /* ======================================================================================= */
 static _Thread_local char g_err[256];
 
-static void set_err(const char* fmt, ...) {
+void bhrt_set_err(const char* fmt, ...) {
     va_list ap;
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof g_err, fmt, ap);
     va_end(ap);
     if (getenv("BHRT_VERBOSE")) fprintf(stderr, "libbhrt: %s\n", g_err);
 }
+#define set_err bhrt_set_err
 
 const char* bhrt_last_error(void) { return g_err; }
 
@@ -1067,13 +1069,6 @@ out:
 /* ======================================================================================= */
 /* context API (src/blackhole_api.c)                                                       */
 /* ======================================================================================= */
-struct BHContext_t {
-    BlackHoleParams blackhole;
-    AccretionDiskParams disk;
-    SimulationConfig config;
-    int disk_enabled;
-};
-
 BHContextHandle bh_initialize(void) { /* blackhole_api.c:52-80 */
     BHContextHandle c = (BHContextHandle)calloc(1, sizeof(struct BHContext_t));
     if (!c) return NULL;

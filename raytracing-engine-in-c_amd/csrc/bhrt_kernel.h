@@ -68,6 +68,19 @@ typedef struct {
                                 [7] redo queue head; zeroed per launch */
 } bhrt_kparams;
 
+/* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and
+ * SimulationConfig of the call */
+typedef struct {
+    double M, rs, a, r_plus; /* mass, schwarzschild_radius, spin * mass, r_plus */
+    double dt;               /* config->time_step                                 */
+    int spin0;               /* blackhole->spin == 0.0                            */
+} bhrt_particle_k;
+
+/* particles.hip: `steps` updates of d_particles[0, count) on `stream`, ev0/ev1 (hipEvent_t,
+ * may be NULL) recorded around the kernel; returns 0 or a hipError_t value. */
+int bhrt_launch_particles(Particle* d_particles, int count, const bhrt_particle_k* k, int steps,
+                          void* stream, void* ev0, void* ev1);
+
 /* launch helpers implemented in geodesic.hip; return 0 or a hipError_t value.
  * bhrt_launch_trace records ev0/ev1 (hipEvent_t, may be NULL) around the trace kernel
  * itself, not the set-up or colour passes. */

@@ -372,7 +372,7 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
 }
 
 // spherical_to_cartesian (spacetime.c:229-237)
-__device__ __forceinline__ void sph2cart(double r, double th, double ph, double& x, double& y,
+__device__ __forceinline__ __attribute__((unused)) void sph2cart(double r, double th, double ph, double& x, double& y,
                                          double& z, Counters* hc) {
     double st, ct, sp, cp;
     bhrt_sincos(th, &st, &ct, hc);

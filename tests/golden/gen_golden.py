@@ -315,7 +315,190 @@ def paths():
     save("paths", **out)
 
 
+LIBC = C.CDLL("libc.so.6")
+PARTICLE_TESTS = [  # position, velocity, mass: geodesic (r < 20 rs), Newtonian, infall, pole
+    ((10.0, 0.0, 0.0), (0.0, 0.3, 0.05), 1.0),
+    ((0.0, 25.0, 3.0), (-0.2, 0.0, 0.1), 1.0),
+    ((30.0, 30.0, 5.0), (0.0, 0.1, 0.0), 0.5),
+    ((3.0, 0.0, 0.0), (-0.5, 0.0, 0.0), 1.0),
+    ((0.0, 0.0, 15.0), (0.1, 0.0, 0.0), 1.0),
+    ((5.0, 5.0, 5.0), (0.0, 0.0, 0.0), 0.0),
+    ((60.0, -10.0, 2.0), (0.0, 0.12, 0.01), 2.0),
+    ((-7.0, 4.0, -2.0), (0.05, 0.2, -0.1), 1.0),
+]
+PARTICLE_STEPS = (1, 10, 60)
+
+
+def particle_arrays(ps):
+    a = abi.particles_view(ps)
+    return {"pos": a["position"].copy(), "vel": a["velocity"].copy(), "type": a["type"].copy(),
+            "active": a["active"].copy(), "id": a["id"].copy(), "age": a["age"].copy(),
+            "temp": a["temperature"].copy(), "mass": a["mass"].copy(),
+            "tdil": a["time_dilation"].copy()}
+
+
+def particles():
+    """particle_sim.c through the reference: seeded creation (srand, then create_accretion_disk
+    and generate_hawking_radiation draw rand() as the reference does), test particles, and
+    update_particles snapshots; plus the visualizer's bh_* sequence (renderer.cpp:879-1005).
+    Fields the reference never initialises (acceleration, energy, ..., time_dilation before
+    the first geodesic step) are set to 0 / -1 by this script before the first update."""
+    P_ = P(abi.ParticleSystem)
+    L.particle_system_init.argtypes = [P_, C.c_int]
+    L.create_accretion_disk.argtypes = [P_, P(abi.BlackHoleParams), P(abi.AccretionDiskParams),
+                                        C.c_int]
+    L.generate_hawking_radiation.argtypes = [P_, P(abi.BlackHoleParams), C.c_int,
+                                             P(abi.SimulationConfig)]
+    L.add_particle.argtypes = [P_, P(abi.Vector3D), P(abi.Vector3D), C.c_double, C.c_int]
+    L.update_particles.argtypes = [P_, P(abi.BlackHoleParams), P(abi.SimulationConfig)]
+    L.particle_system_cleanup.argtypes = [P_]
+    out = {}
+    cases = [(0.0, 1234, 200, 40, 0.1), (0.9, 99, 64, 16, 0.05)]  # spin, seed, disk, hawking, dt
+    for ci, (spin, seed, n_disk, n_hawk, dt) in enumerate(cases):
+        bh = ref_black_hole(1.0, spin)
+        dk = abi.disk(bh.isco_radius, 20.0, 1.0, 1.0)
+        dk.thickness_factor = 0.1
+        cfg = abi.sim_config(dt, 100.0, 1000, 1e-6)
+        cfg.hawking_temp_factor = 1.0
+        ps = abi.ParticleSystem()
+        assert L.particle_system_init(C.byref(ps), 400) == 0
+        LIBC.srand(seed)
+        made = [L.create_accretion_disk(C.byref(ps), C.byref(bh), C.byref(dk), n_disk),
+                L.generate_hawking_radiation(C.byref(ps), C.byref(bh), n_hawk, C.byref(cfg))]
+        for pos, vel, m in PARTICLE_TESTS:
+            made.append(L.add_particle(C.byref(ps), C.byref(abi.v3(*pos)), C.byref(abi.v3(*vel)),
+                                       m, abi.PARTICLE_TEST))
+        a = abi.particles_view(ps)
+        for f in ("acceleration", "energy", "angular_momentum", "proper_time", "coordinate_time"):
+            a[f] = 0.0
+        a["time_dilation"] = -1.0
+        pre = f"case{ci}_"
+        out[pre + "in"] = np.array([spin, seed, n_disk, n_hawk, dt, ps.count])
+        out[pre + "made"] = np.array(made)
+        out[pre + "bh"] = np.array([getattr(bh, f) for f, _ in abi.BlackHoleParams._fields_])
+        out[pre + "disk"] = np.array([getattr(dk, f) for f, _ in abi.AccretionDiskParams._fields_])
+        for k, v in particle_arrays(ps).items():
+            out[pre + "init_" + k] = v
+        done = 0
+        for s_ in PARTICLE_STEPS:
+            while done < s_:
+                assert L.update_particles(C.byref(ps), C.byref(bh), C.byref(cfg)) == 0
+                done += 1
+            for k, v in particle_arrays(ps).items():
+                out[pre + f"s{s_}_" + k] = v
+        L.particle_system_cleanup(C.byref(ps))
+    out["ncases"] = np.array(len(cases))
+    out["steps"] = np.array(PARTICLE_STEPS)
+    out["tests"] = np.array([list(p) + list(v) + [m] for p, v, m in PARTICLE_TESTS])
+
+    # the visualizer's per-frame sequence through the context API
+    L.bh_initialize.restype = C.c_void_p
+    L.bh_create_particle_system.restype = C.c_void_p
+    L.bh_create_particle_system.argtypes = [C.c_void_p, C.c_int]
+    for f in ("bh_configure_black_hole",):
+        getattr(L, f).argtypes = [C.c_void_p, C.c_double, C.c_double, C.c_double]
+    L.bh_configure_accretion_disk.argtypes = [C.c_void_p] + [C.c_double] * 4
+    L.bh_configure_simulation.argtypes = [C.c_void_p, C.c_double, C.c_double, C.c_int,
+                                          C.c_double]
+    L.bh_create_accretion_disk_particles.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    L.bh_update_particles.argtypes = [C.c_void_p, C.c_void_p]
+    L.bh_get_particle_data.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, P(C.c_int)]
+    L.bh_destroy_particle_system.argtypes = [C.c_void_p, C.c_void_p]
+    L.bh_shutdown.argtypes = [C.c_void_p]
+    ctx = L.bh_initialize()
+    assert L.bh_configure_black_hole(ctx, 1.0, 0.0, 0.0) == 0
+    assert L.bh_configure_accretion_disk(ctx, 6.0, 20.0, 1.0, 1.0) == 0
+    assert L.bh_configure_simulation(ctx, 0.05, 100.0, 1000, 1e-6) == 0
+    sysp = L.bh_create_particle_system(ctx, 5000)
+    LIBC.srand(777)
+    made = L.bh_create_accretion_disk_particles(ctx, sysp, 3000)
+    for _ in range(5):
+        assert L.bh_update_particles(ctx, sysp) == 0
+    pos = np.zeros(5000 * 3)
+    vel = np.zeros(5000 * 3)
+    typ = np.zeros(5000, dtype=np.int32)
+    cnt = C.c_int(5000)
+    rc = L.bh_get_particle_data(ctx, sysp, pos.ctypes.data, vel.ctypes.data, typ.ctypes.data,
+                                C.byref(cnt))
+    L.bh_destroy_particle_system(ctx, sysp)
+    L.bh_shutdown(ctx)
+    n = cnt.value
+    out["viz_made"] = np.array([made, rc, n])
+    out["viz_pos"] = pos[:3 * n].reshape(n, 3)
+    out["viz_vel"] = vel[:3 * n].reshape(n, 3)
+    out["viz_type"] = typ[:n]
+    save("particles", **out)
+
+
+def spacetime_helpers():
+    """The scalar metric helpers of spacetime.h (spacetime.c:38-187, 242-327, 377-656) on a
+    grid of inputs; libbhrt restates them on the host (kerr_helpers.c, particles.c)."""
+    D, I, V = C.c_double, C.c_int, C.c_void_p
+    sig = {"calculate_effective_potential": ([D, D, V], D),
+           "calculate_ergosphere_radius": ([D, V], D),
+           "calculate_kerr_metric_bl": ([V, D, D, V], I),
+           "calculate_inverse_kerr_metric": ([V, D, D, V], I),
+           "calculate_kerr_christoffel": ([V, D, D, V], I),
+           "calculate_kerr_isco": ([D, D, C.c_bool], D),
+           "calculate_kerr_event_horizon": ([D, D], D),
+           "calculate_kerr_ergosphere": ([D, D, D], D),
+           "calculate_frame_dragging": ([V, D, D, V], I),
+           "calculate_kerr_geodesic": ([V, V, D, D, V], I),
+           "calculate_christoffel_symbols": ([D, D, V, V], None),
+           "geodesic_equation": ([V, V, V, V], None)}
+    for f, (a, r) in sig.items():
+        getattr(L, f).argtypes, getattr(L, f).restype = a, r
+    rng = np.random.default_rng(11)
+    n = 48
+    r = np.concatenate([[2.0, 2.0000000001, 1.5, 3.0, 6.0], rng.uniform(1.0, 60.0, n - 5)])
+    th = np.concatenate([[0.0, np.pi / 2, np.pi, 1e-9, 1.0], rng.uniform(0.0, np.pi, n - 5)])
+    l = rng.uniform(-6.0, 6.0, n)
+    vel = rng.normal(size=(n, 4))
+    out = {"r": r, "th": th, "l": l, "vel": vel, "spins": np.array([0.0, 0.5, 0.9, 0.99])}
+    for si, spin in enumerate(out["spins"]):
+        bh = ref_black_hole(1.0, spin)
+        a = spin
+        res = {k: [] for k in ("veff", "ergo", "bl", "inv", "kchr", "isco", "hor", "kergo",
+                               "drag", "kgeo", "chr", "geo", "rc")}
+        for i in range(n):
+            pos = np.array([0.0, r[i], th[i], 0.3])
+            km = (D * 7)()
+            res["veff"].append(L.calculate_effective_potential(r[i], l[i], C.byref(bh)))
+            res["ergo"].append(L.calculate_ergosphere_radius(th[i], C.byref(bh)))
+            rc = [L.calculate_kerr_metric_bl(pos.ctypes.data, a, 1.0, km)]
+            res["bl"].append([km[0], km[1], km[2], km[4], km[5]])
+            rc.append(L.calculate_inverse_kerr_metric(pos.ctypes.data, a, 1.0, km))
+            res["inv"].append([km[0], km[1], km[2], km[4], km[5]])
+            G = np.zeros(64)
+            rc.append(L.calculate_kerr_christoffel(pos.ctypes.data, a, 1.0, G.ctypes.data))
+            res["kchr"].append(G.copy())
+            res["isco"].append([L.calculate_kerr_isco(a, 1.0, True),
+                                L.calculate_kerr_isco(a, 1.0, False)])
+            res["hor"].append(L.calculate_kerr_event_horizon(a, 1.0))
+            res["kergo"].append(L.calculate_kerr_ergosphere(a, 1.0, th[i]))
+            v3 = np.zeros(3)
+            rc.append(L.calculate_frame_dragging(pos.ctypes.data, a, 1.0, v3.ctypes.data))
+            res["drag"].append(v3)
+            acc = np.zeros(4)
+            rc.append(L.calculate_kerr_geodesic(pos.ctypes.data, vel[i].ctypes.data, a, 1.0,
+                                                acc.ctypes.data))
+            res["kgeo"].append(acc)
+            G2 = np.zeros(64)
+            L.calculate_christoffel_symbols(r[i], th[i], C.byref(bh), G2.ctypes.data)
+            res["chr"].append(G2)
+            acc2 = np.zeros(4)
+            L.geodesic_equation(pos.ctypes.data, vel[i].ctypes.data, C.byref(bh), acc2.ctypes.data)
+            res["geo"].append(acc2)
+            res["rc"].append(rc)
+        for k, v in res.items():
+            out[f"s{si}_{k}"] = np.array(v)
+    save("spacetime_helpers", **out)
+
+
 if __name__ == "__main__":
+    spacetime_helpers()
+    particles()
     kat_main()
     shading()
     pixels()
