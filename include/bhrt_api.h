@@ -236,6 +236,10 @@ typedef struct {
     double*  rgb_r;         /* frame colour contract, DESIGN.md section 3                */
     double*  rgb_g;
     double*  rgb_b;
+    /* display path (renderer.cpp:2090-2125, the visualizer's texture buffer): 4 values per
+     * pixel, row 0 = top image row */
+    float*   rgba32f;       /* (float)rgb and alpha 1.0f: the compute shader's RayOutput   */
+    uint8_t* rgba8;         /* (unsigned char)(std::min(1.0f, v) * 255.0f) of rgba32f      */
 } bhrt_frame_soa;
 
 /* Cyclic row-block sharding of an image across num_shards GPUs: block b (rows

@@ -88,10 +88,13 @@ class Rows(C.Structure):
 SOA_FIELDS = ("result", "steps", "hit_x", "hit_y", "hit_z", "distance", "time_dilation",
               "sky_x", "sky_y", "sky_z", "rgb_r", "rgb_g", "rgb_b")
 SOA_DTYPES = {f: (np.int32 if f in ("result", "steps") else np.float64) for f in SOA_FIELDS}
+# display path: 4 values per pixel (bhrt_frame_soa.rgba32f / rgba8)
+DISPLAY_FIELDS = ("rgba32f", "rgba8")
+SOA_DTYPES.update(rgba32f=np.float32, rgba8=np.uint8)
 
 
 class FrameSoA(C.Structure):
-    _fields_ = [(f, C.c_void_p) for f in SOA_FIELDS]
+    _fields_ = [(f, C.c_void_p) for f in SOA_FIELDS + DISPLAY_FIELDS]
 
 
 class Stats(C.Structure):
@@ -158,7 +161,8 @@ def v3(x, y, z):
 
 def alloc_soa(n, fields=SOA_FIELDS):
     """Host SoA arrays (numpy) + the FrameSoA struct pointing at them."""
-    arrays = {f: np.zeros(n, dtype=SOA_DTYPES[f]) for f in fields}
+    arrays = {f: np.zeros((n, 4) if f in DISPLAY_FIELDS else n, dtype=SOA_DTYPES[f])
+              for f in fields}
     soa = FrameSoA(**{f: a.ctypes.data for f, a in arrays.items()})
     return arrays, soa
 

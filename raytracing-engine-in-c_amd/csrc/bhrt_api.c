@@ -88,7 +88,7 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 #define BHRT_MAX_DEV 16
 #define BHRT_RING 64        /* control blocks per context             */
 #define BHRT_CTL_WORDS 8    /* u64 per control block (64 B)           */
-#define BHRT_NFIELDS 13
+#define BHRT_NFIELDS 15
 
 typedef struct {
     int slot;
@@ -380,6 +380,19 @@ static int check_scene(const BlackHoleParams* bh, const SimulationConfig* cfg) {
     return 0;
 }
 
+/* the colour pass (rgb and/or the display fields) reads result and the hit point */
+static int colour_args_bad(const bhrt_frame_soa* out) {
+    if ((out->rgb_r || out->rgb_g || out->rgb_b) && !(out->rgb_r && out->rgb_g && out->rgb_b)) {
+        set_err("rgb output needs all of rgb_r/g/b");
+        return 1;
+    }
+    if ((out->rgb_r || out->rgba32f || out->rgba8) && (!out->result || !out->hit_x || !out->hit_y)) {
+        set_err("colour outputs need result and hit_x/hit_y");
+        return 1;
+    }
+    return 0;
+}
+
 int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParams* dk,
                              const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
                              const bhrt_rows* rows, IntegrationMethod method, int flags,
@@ -396,10 +409,7 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
     int dev = current_device();
     devctx_t* c = ctx_get(dev);
     if (!c) return -1;
-    if (out->rgb_r && (!out->rgb_g || !out->rgb_b || !out->result || !out->hit_x || !out->hit_y)) {
-        set_err("rgb output needs rgb_r/g/b, result and hit_x/hit_y");
-        return -1;
-    }
+    if (colour_args_bad(out)) return -1;
     if (ensure(&c->d_init, &c->cap_init,
                (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) * (size_t)nrows * (size_t)W, 0))
         return -1;
@@ -421,10 +431,7 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
         if (!g_err[0]) set_err("invalid argument");
         return -1;
     }
-    if (out->rgb_r && (!out->rgb_g || !out->rgb_b || !out->result || !out->hit_x || !out->hit_y)) {
-        set_err("rgb output needs rgb_r/g/b, result and hit_x/hit_y");
-        return -1;
-    }
+    if (colour_args_bad(out)) return -1;
     devctx_t* c = ctx_get(current_device());
     if (!c) return -1;
     if (ensure(&c->d_init, &c->cap_init,
@@ -441,7 +448,7 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
 }
 
 /* ---- host-buffer paths: device SoA block <-> caller SoA ---- */
-static const size_t k_fsize[BHRT_NFIELDS] = {4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
+static const size_t k_fsize[BHRT_NFIELDS] = {4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 16, 4};
 
 static void** soa_slot(bhrt_frame_soa* s, int f) { return ((void**)s) + f; }
 
@@ -449,8 +456,9 @@ static void** soa_slot(bhrt_frame_soa* s, int f) { return ((void**)s) + f; }
 static int device_soa(devctx_t* c, long n, const bhrt_frame_soa* want_in, bhrt_frame_soa* dev) {
     bhrt_frame_soa want_buf = *want_in;
     const bhrt_frame_soa* want = &want_buf;
-    if (want_buf.rgb_r || want_buf.rgb_g || want_buf.rgb_b) { /* the colour pass reads these */
+    if (want_buf.rgb_r || want_buf.rgb_g || want_buf.rgb_b) /* written together */
         want_buf.rgb_r = want_buf.rgb_g = want_buf.rgb_b = (double*)1;
+    if (want_buf.rgb_r || want_buf.rgba32f || want_buf.rgba8) { /* the colour pass reads these */
         if (!want_buf.result) want_buf.result = (int32_t*)1;
         if (!want_buf.hit_x) want_buf.hit_x = (double*)1;
         if (!want_buf.hit_y) want_buf.hit_y = (double*)1;

@@ -836,6 +836,13 @@ __device__ __forceinline__ double clampd(double v, double lo, double hi) {
 // Frame colour contract, one elementwise pass after the trace:
 // calculate_disk_temperature + temperature_to_rgb (+ apply_relativistic_effects) for disk
 // hits, black for the horizon, the sky gradient of raytracer.c:1150-1157 otherwise.
+// (unsigned char)(std::min(1.0f, v) * 255.0f) as the visualizer's x86 build evaluates it:
+// std::min keeps 1.0f for NaN, the cast truncates toward zero and keeps the low byte.
+__device__ __forceinline__ unsigned to_u8(float v) {
+    const float m = (v < 1.0f) ? v : 1.0f;
+    return (unsigned)(int)(m * 255.0f) & 0xffu;
+}
+
 template <int SRC>
 __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
     const Scene& sc = kp.sc;
@@ -891,9 +898,18 @@ __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
             g = (1.0 - t) * 1.0 + t * 0.7;
             b = (1.0 - t) * 1.0 + t * 1.0;
         }
-        s.rgb_r[i] = r;
-        s.rgb_g[i] = g;
-        s.rgb_b[i] = b;
+        if (s.rgb_r) {
+            s.rgb_r[i] = r;
+            s.rgb_g[i] = g;
+            s.rgb_b[i] = b;
+        }
+        if (s.rgba32f || s.rgba8) {  // the display path (renderer.cpp:2090-2125)
+            const float fr = (float)r, fg = (float)g, fb = (float)b;
+            if (s.rgba32f) reinterpret_cast<float4*>(s.rgba32f)[i] = make_float4(fr, fg, fb, 1.0f);
+            if (s.rgba8)
+                reinterpret_cast<unsigned*>(s.rgba8)[i] =
+                    to_u8(fr) | (to_u8(fg) << 8) | (to_u8(fb) << 16) | (to_u8(1.0f) << 24);
+        }
     }
 }
 
@@ -976,7 +992,7 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
     k_trace<METHOD, DISK, SPIN0, FAR, true><<<blocks < grid_huge ? blocks : grid_huge, 256, 0,
                                               st>>>(kp);
     if (ev1) (void)hipEventRecord(ev1, st);
-    if (kp.out.rgb_r) {
+    if (kp.out.rgb_r || kp.out.rgba32f || kp.out.rgba8) {
         if (kp.src == BHRT_SRC_CAMERA)
             k_colour<BHRT_SRC_CAMERA><<<grid_for(reinterpret_cast<const void*>(&k_colour<BHRT_SRC_CAMERA>),
                                                  kp.n), 256, 0, st>>>(kp);

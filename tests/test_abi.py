@@ -49,6 +49,8 @@ def test_reference_entry_points_are_declared():
 
 
 def test_struct_layouts():
+    assert C.sizeof(abi.FrameSoA) == 15 * 8  # 13 per-ray fields + 2 display fields
+    assert abi.FrameSoA.rgba8.offset == 14 * 8
     assert C.sizeof(abi.RayTraceHit) == 160 == abi.HIT_DTYPE.itemsize
     assert C.sizeof(abi.Ray) == 48 == abi.RAY_DTYPE.itemsize
     assert C.sizeof(abi.SimulationConfig) == 72

@@ -334,3 +334,40 @@ def test_large_argument_rays_take_the_redo_path(bhrt_lib, oracle):
         compare(got, want, RTOL, False, "large-argument rays")
         assert st["rays"] == len(sel)
         assert st["rays_redone"] > 0, st
+
+
+def _display_u8(v):
+    """(unsigned char)(std::min(1.0f, v) * 255.0f), renderer.cpp:2113-2116, on x86."""
+    v = v.astype(np.float32)
+    m = np.where(v < np.float32(1.0), v, np.float32(1.0)).astype(np.float32)
+    with np.errstate(invalid="ignore"):
+        return (np.trunc(m * np.float32(255.0)).astype(np.int64) & 0xFF).astype(np.uint8)
+
+
+@pytest.mark.parametrize("cname", ["C2", "C4"])
+def test_display_path_rgba(bhrt_lib, oracle, cname):
+    """the visualizer's texture buffer (float RGBA with alpha 1, then
+    RGBA8 by its own conversion) produced by the colour pass, row 0 = top."""
+    c = configs.CONFIGS[cname]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera("B")
+    W, H = 96, 54
+    fields = abi.SOA_FIELDS + abi.DISPLAY_FIELDS
+    got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags, fields=fields)
+    rgb = np.stack([got["rgb_r"], got["rgb_g"], got["rgb_b"]], axis=1)
+    f32 = got["rgba32f"]
+    assert np.array_equal(f32[:, :3], rgb.astype(np.float32), equal_nan=True)
+    assert (f32[:, 3] == 1.0).all()
+    assert np.array_equal(got["rgba8"], _display_u8(f32))
+    # the display fields alone (no per-ray outputs requested) give the same image
+    only = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags,
+                                 fields=abi.DISPLAY_FIELDS)
+    assert np.array_equal(only["rgba8"], got["rgba8"])
+    assert np.array_equal(only["rgba32f"], f32, equal_nan=True)
+    # and the colours are the oracle's (frame colour contract) to the float32 rounding
+    want = oracle.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+    w32 = np.stack([want["rgb_r"], want["rgb_g"], want["rgb_b"]], axis=1).astype(np.float32)
+    ok = ~np.isnan(w32)
+    assert np.array_equal(np.isnan(f32[:, :3]), ~ok)
+    np.testing.assert_allclose(f32[:, :3][ok], w32[ok], rtol=1e-5, atol=1e-6)
+    assert np.abs(got["rgba8"][:, :3].astype(int) - _display_u8(w32).astype(int)).max() <= 1
