@@ -1,14 +1,21 @@
 """Benchmark of the geodesic ray-tracing hot path (BASELINE.json metric) on MI355X.
 
 One "step" = one camera frame of the workload traced by libbhrt.so with every input already
-on the device: the frame kernel launch, plus (N > 1) the single RCCL gather of all shards to
-rank 0 and the device-side un-permute of the cyclic row blocks into the final image.
+on the device: the frame kernel launch, plus (N > 1) the single RCCL gather of all ranks'
+buffers to rank 0 and its assembly there (bhrt/dist_frame.py FramePipeline; the gather of
+frame i overlaps the rendering of frame i+1, and the timed region ends after the last one).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--camera B]
 
-N > 1 is launched by torch.distributed.run, one process per GPU. Weak scaling: every GPU owns
-a full configuration-sized shard (1920 x 1080 pixels for C2) of an image 1080*N rows tall,
-assigned as cyclic 8-row blocks so the divergent disk band spreads evenly.
+N > 1 is launched by torch.distributed.run, one process per GPU.
+  * Weak scaling (C1, C2, C3, C5): every GPU traces the whole configuration frame (1920 x 1080
+    for C2) at its own sub-pixel offset -- rank 0 the pixel centres, rank k the reference's
+    Halton sample k (trace_pixel's jitter) -- so N GPUs supersample the frame with N samples
+    per pixel and every GPU does exactly one frame's work; rank 0 averages the colour.
+    (A taller image 1080*N rows high is NOT used: with the fixed vertical FOV its horizontal
+    FOV shrinks with N and the per-ray work collapses -- 400 -> 1.6 iterations/ray at N=8.)
+  * Strong scaling (C4): one 3840 x 2160 image split into cyclic 8-row blocks (block b ->
+    rank b % N), un-permuted on rank 0 after the gather.
 
 The JSON line also carries:
   roofline      FP64 VALU roofline of the trace kernel: algorithmic FLOPs (SURVEY.md 8(a):
@@ -32,7 +39,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from bhrt import abi, configs, lib  # noqa: E402
-from bhrt.dist_frame import FrameBuffer, gather_frame  # noqa: E402
+from bhrt.dist_frame import FramePipeline, sample_offset  # noqa: E402
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (and FP64 matrix) peak, AMD spec
 METRIC = "Mrays/s (and RK4 steps/s) per GPU + per node; max |Δhit| vs CPU ref"
@@ -51,6 +58,9 @@ def parse():
     p.add_argument("--cpu-rows-stride", type=int, default=27,
                    help="CPU baseline samples every k-th image row")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--sample", type=int, default=None,
+                   help="weak scaling: trace sample plane K instead of this rank's (to time "
+                        "each plane of an N-GPU run on one GPU)")
     return p.parse_args()
 
 
@@ -77,23 +87,30 @@ def main():
     c = configs.CONFIGS[args.config]
     bh, dk, cfg = c.scene()
     cam = configs.camera(args.camera)
-    W, H = c.width, c.bench_height(world)
-    rows = abi.Rows(ROW_BLOCK, rank, world)
-    n_rows = lib.shard_rows(H, rows)
-    n = n_rows * W
-    frame = FrameBuffer(n, device)
-    soa = frame.soa()
+    strong = c.scaling == "strong"
+    W, H = c.width, c.bench_height(1)
+    if strong:
+        rows = abi.Rows(ROW_BLOCK, rank, world) if world > 1 else None
+        n = lib.shard_rows(H, rows) * W
+    else:
+        rows = None
+        n = W * H
+        off = sample_offset(rank if args.sample is None else args.sample)
+        if off is not None:
+            cam.use_offset, cam.offset_x, cam.offset_y = 1, off[0], off[1]
+    pipe = FramePipeline(n, device, world, rank, "shards" if strong else "samples", H, W,
+                         ROW_BLOCK, FIELDS)
     stream = torch.cuda.current_stream()
-    gathered = [torch.empty_like(frame.buf) for _ in range(world)] if (world > 1 and rank == 0) else None
 
     def step():
-        lib.render_frame_device(bh, dk, cfg, cam, W, H, rows if world > 1 else None, c.method,
-                                c.flags, soa, stream.cuda_stream)
-        # one RCCL gather of the packed shards + un-permute into the H x W image on rank 0
-        return gather_frame(frame, H, W, ROW_BLOCK, world, rank, gathered)
+        fb = pipe.next_buffer()
+        lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags, fb.soa(),
+                                stream.cuda_stream)
+        pipe.submit()
 
     for _ in range(args.warmup):
         step()
+    pipe.finish()
     torch.cuda.synchronize()
     lib.stats(reset=True)
     if world > 1:
@@ -102,6 +119,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    frame = pipe.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -121,7 +139,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    rays_all = float(W * H) * args.steps
+    rays_all = float(W * H) * args.steps * (1 if strong else world)
     mrays = rays_all / elapsed / 1e6
     kern_ms = st["kernel_ms"] / max(st["launches"], 1)
     f_launch = flops(st, c.method) / max(st["launches"], 1)
@@ -142,11 +160,17 @@ def main():
         "config": {
             "workload": f"{c.name}: {c.note}",
             "camera": args.camera,
+            "sample_plane": None if strong else (rank if args.sample is None else args.sample),
             "width": W,
             "height": H,
             "rays_per_gpu": n,
-            "parallelism": (f"dp{world}: cyclic {ROW_BLOCK}-row blocks, one RCCL gather to rank 0"
-                            if world > 1 else "single GPU"),
+            "parallelism": ("single GPU" if world == 1 else
+                            (f"dp{world}: cyclic {ROW_BLOCK}-row blocks of one image, one RCCL "
+                             "gather to rank 0 per frame (overlapped with the next frame)")
+                            if strong else
+                            (f"dp{world}: one sub-pixel sample plane of the frame per GPU "
+                             f"({world} samples/pixel), one RCCL gather to rank 0 per frame "
+                             "(overlapped with the next frame)")),
         },
         "rk4_steps_per_s": round(iterations_all * (1.0 / elapsed), 1),
         "per_gpu_mrays_s": round(mrays / world, 3),
@@ -210,7 +234,7 @@ def cpu_baseline(args, c, bh, dk, cfg, cam, frame):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     W, H = c.width, c.bench_height(1)
     rows = list(range(0, H, args.cpu_rows_stride))
-    got = {f: frame.views[f].view(-1).cpu().numpy().reshape(H, W)[rows] for f in FIELDS}
+    got = {f: frame[f].reshape(H, W).cpu().numpy()[rows] for f in FIELDS}
     t0 = time.perf_counter()
     want = []
     for r in rows:

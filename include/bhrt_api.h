@@ -207,12 +207,16 @@ BHErrorCode bh_generate_shader_data(void* context, const float observer_pos[3],
 /* ================================ 2. bhrt extension ===================================== */
 
 /* Pinhole camera of trace_pixel/calculate_ray_direction (raytracer.c:999-1039); fov in
- * degrees; pixel-centre rays (offset 0.5, 0.5). */
+ * degrees. Rays go through the pixel centres (offset 0.5, 0.5) unless use_offset is set:
+ * then every pixel uses (offset_x, offset_y), e.g. one sample of trace_pixel's jitter
+ * (generate_jittered_position, raytracer.c:868-932). A zero-initialised tail means centres. */
 typedef struct {
     Vector3D position;
     Vector3D direction;
     Vector3D up;
     double   fov_deg;
+    int      use_offset;
+    double   offset_x, offset_y;
 } bhrt_camera;
 
 /* Frame flags */

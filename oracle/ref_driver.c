@@ -141,7 +141,8 @@ int refdrv_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* di
     for (long i = 0; i < n; i++) {
         int x = (int)(i % W), y = orc_shard_row((int)(i / W), rows);
         Vector3D dir;
-        orc_camera_ray_direction(x, y, 0.5, 0.5, W, H, cam, &dir);
+        orc_camera_ray_direction(x, y, cam->use_offset ? cam->offset_x : 0.5,
+                                 cam->use_offset ? cam->offset_y : 0.5, W, H, cam, &dir);
         Ray ray = {cam->position, dir};
         RayTraceHit h;
         memset(&h, 0, sizeof h);

@@ -78,7 +78,8 @@ class GPUShaderParams(C.Structure):
 
 class Camera(C.Structure):
     _fields_ = [("position", Vector3D), ("direction", Vector3D), ("up", Vector3D),
-                ("fov_deg", C.c_double)]
+                ("fov_deg", C.c_double), ("use_offset", C.c_int), ("offset_x", C.c_double),
+                ("offset_y", C.c_double)]
 
 
 class Rows(C.Structure):

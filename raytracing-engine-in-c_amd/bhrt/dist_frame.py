@@ -1,10 +1,19 @@
-"""Multi-GPU frame assembly: one shard per rank, one gather, one un-permute.
+"""Multi-GPU frame assembly: one buffer per rank, one gather per frame, pipelined.
 
-The image is split into cyclic row blocks (block b -> rank b % world; bhrt_rows in
-include/bhrt_api.h), so the divergent disk band lands on every GPU. Each rank renders its
-rows into ONE contiguous byte buffer holding every SoA field (FrameBuffer), so assembling
-the frame is a single collective (torch.distributed.gather: RCCL on GPUs, gloo in the CPU
-tests) followed by a device-side permutation back to image order.
+Each rank renders into ONE contiguous byte buffer holding every SoA field (FrameBuffer), so
+assembling a frame on rank 0 is a single collective (torch.distributed.gather: RCCL on GPUs,
+gloo in the CPU tests). Two ways of splitting the work (FramePipeline.mode):
+
+  * "shards" (strong scaling, one image): cyclic row blocks (block b -> rank b % world;
+    bhrt_rows in include/bhrt_api.h), so the divergent disk band lands on every GPU; rank 0
+    permutes the gathered shards back to image order on the device.
+  * "samples" (weak scaling): every rank traces the whole frame at its own sub-pixel offset
+    (sample_offset: rank 0 the pixel centre, rank k the reference's Halton point k), i.e.
+    the frame is supersampled across GPUs with the per-GPU work of one frame; rank 0 keeps
+    the per-sample planes and averages their colour.
+
+The gather of frame i runs (on the collective's own stream) while frame i+1 renders; a
+buffer is reused only after the gather that read it has completed (double buffering).
 """
 import numpy as np
 import torch
@@ -77,3 +86,84 @@ def gather_frame(fb, H, W, row_block, world, rank, gathered=None):
         img[f] = (parts.view(world, n_rows // row_block, row_block, W)
                   .permute(1, 0, 2, 3).reshape(H, W))
     return img
+
+
+def sample_offset(k):
+    """Sub-pixel offset of sample plane k: None (pixel centre) for k = 0, else the Halton
+    point of generate_jittered_position's JITTER_HALTON (raytracer.c:900-915)."""
+    if k == 0:
+        return None
+    from . import lib
+    return lib.halton(k, 2), lib.halton(k, 3)
+
+
+class FramePipeline:
+    """Double-buffered render -> gather-to-rank-0 -> assemble.
+
+    Per frame: fb = next_buffer(); render into fb; submit(). finish() completes the gathers
+    still in flight and returns rank 0's newest assembled frame (None elsewhere):
+      shards:  {field: [H, W]}
+      samples: {field: [world, H, W]} plus "rgb_mean" [3, H, W] when rgb was rendered.
+    """
+
+    def __init__(self, n, device, world, rank, mode, H, W, row_block=8,
+                 fields=abi.SOA_FIELDS):
+        assert mode in ("shards", "samples")
+        self.world, self.rank, self.mode = world, rank, mode
+        self.H, self.W, self.row_block = H, W, row_block
+        self.bufs = [FrameBuffer(n, device, fields) for _ in range(2)]
+        self.gathered = ([[torch.empty_like(b.buf) for _ in range(world)] for b in self.bufs]
+                         if (world > 1 and rank == 0) else None)
+        self.works = [None, None]
+        self.frames = 0
+        self.last = None
+
+    def next_buffer(self):
+        slot = self.frames % 2
+        self._complete(slot)
+        return self.bufs[slot]
+
+    def submit(self):
+        slot = self.frames % 2
+        if self.world > 1:
+            self.works[slot] = dist.gather(
+                self.bufs[slot].buf, self.gathered[slot] if self.rank == 0 else None, dst=0,
+                async_op=True)
+        else:
+            self.works[slot] = True
+        self.frames += 1
+
+    def finish(self):
+        for k in range(max(self.frames - 2, 0), self.frames):  # oldest first
+            self._complete(k % 2)
+        return self.last
+
+    def _complete(self, slot):
+        w = self.works[slot]
+        if w is None:
+            return
+        if w is not True:
+            w.wait()
+        self.works[slot] = None
+        if self.rank == 0:
+            self.last = self._assemble(slot)
+
+    def _assemble(self, slot):
+        fb, H, W, world = self.bufs[slot], self.H, self.W, self.world
+        parts = self.gathered[slot] if world > 1 else [fb.buf]
+        img = {}
+        if self.mode == "shards":
+            if world == 1:
+                return {f: fb.views[f].view(H, W) for f in fb.fields}
+            n_rows, B = fb.n // W, self.row_block
+            for f in fb.fields:
+                p = torch.stack([fb.view(g, f) for g in parts])  # [world, n_rows*W]
+                img[f] = p.view(world, n_rows // B, B, W).permute(1, 0, 2, 3).reshape(H, W)
+            return img
+        for f in fb.fields:
+            img[f] = (fb.views[f].view(1, H, W) if world == 1 else
+                      torch.stack([fb.view(g, f) for g in parts]).view(world, H, W))
+        if all(c in img for c in ("rgb_r", "rgb_g", "rgb_b")):
+            img["rgb_mean"] = torch.stack([img[c].mean(dim=0)
+                                           for c in ("rgb_r", "rgb_g", "rgb_b")])
+        return img

@@ -162,3 +162,11 @@ def stats(reset=False):
     s = abi.Stats()
     _check(load().bhrt_get_stats(C.byref(s), 1 if reset else 0), "bhrt_get_stats")
     return {f: getattr(s, f) for f, _ in abi.Stats._fields_}
+
+
+def halton(index, base):
+    """halton_sequence (raytracer.c:852-863), libbhrt's host export."""
+    L = load()
+    L.halton_sequence.restype = C.c_double
+    L.halton_sequence.argtypes = [C.c_int, C.c_int]
+    return L.halton_sequence(index, base)

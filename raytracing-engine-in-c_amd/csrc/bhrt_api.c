@@ -295,6 +295,8 @@ static void fill_camera(bhrt_kparams* kp, const bhrt_camera* cam, int W, int H) 
     k->up[0] = up.x; k->up[1] = up.y; k->up[2] = up.z;
     k->plane_h = plane_h;
     k->plane_w = plane_h * aspect;
+    k->off_x = cam->use_offset ? cam->offset_x : 0.5;
+    k->off_y = cam->use_offset ? cam->offset_y : 0.5;
     k->width = W;
     k->height = H;
     k->pos[0] = cam->position.x;
@@ -811,7 +813,7 @@ RayTraceResult trace_pixel(int px, int py, int W, int H, const Vector3D* cam_pos
             free(rays); free(rgb); free(res);
             return RAY_ERROR;
         }
-        bhrt_camera cam = {*cam_pos, *cam_dir, *cam_up, fov};
+        bhrt_camera cam = {*cam_pos, *cam_dir, *cam_up, fov, 0, 0.0, 0.0};
         bhrt_kparams basis;
         fill_scene(&basis, bh, dk, cfg, INTEGRATOR_RK4, 0);
         fill_camera(&basis, &cam, W, H);

@@ -42,6 +42,7 @@ typedef struct {
     /* pixel -> direction (calculate_ray_direction, raytracer.c:999-1039) */
     double fwd[3], right[3], up[3];
     double plane_w, plane_h;
+    double off_x, off_y;             /* sub-pixel offset (0.5, 0.5 = centre)   */
     int width, height;
     bhrt_rows rows;
     /* shared origin (integrate_photon_path set-up, raytracer.c:355-466) */

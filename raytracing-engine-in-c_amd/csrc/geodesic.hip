@@ -505,8 +505,8 @@ __device__ __forceinline__ void camera_dir(const bhrt_camera_k& cm, int i, doubl
         const int B = cm.rows.row_block;
         py = ((j / B) * cm.rows.num_shards + cm.rows.shard) * B + j % B;
     }
-    const double ndcx = (2.0 * ((px + 0.5) / W) - 1.0) * cm.plane_w;
-    const double ndcy = (1.0 - 2.0 * ((py + 0.5) / cm.height)) * cm.plane_h;
+    const double ndcx = (2.0 * ((px + cm.off_x) / W) - 1.0) * cm.plane_w;
+    const double ndcy = (1.0 - 2.0 * ((py + cm.off_y) / cm.height)) * cm.plane_h;
     double vx = cm.fwd[0], vy = cm.fwd[1], vz = cm.fwd[2];
     vx = vx + cm.right[0] * ndcx;
     vy = vy + cm.right[1] * ndcx;

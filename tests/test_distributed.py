@@ -96,3 +96,75 @@ def test_framebuffer_alignment():
         for f, (a, b) in fb.offsets.items():
             assert a % (4 if f in ("result", "steps") else 8) == 0
             assert b - a == n * (4 if f in ("result", "steps") else 8)
+
+
+def _pipeline_worker(rank, world, port, mode, W, H, frames, out_path):
+    """bench.py's FramePipeline with oracle-rendered frames: `frames` frames in flight
+    through the double-buffered async gathers."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    from bhrt.dist_frame import FramePipeline, sample_offset
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c, bh, dk, cfg, cam = _scene()
+        B = 4
+        if mode == "shards":
+            rows = abi.Rows(B, rank, world)
+            n = shard_row_count(H, B, rank, world) * W
+        else:
+            rows, n = None, W * H
+            off = sample_offset(rank)
+            if off is not None:
+                cam.use_offset, cam.offset_x, cam.offset_y = 1, off[0], off[1]
+        pipe = FramePipeline(n, "cpu", world, rank, mode, H, W, B)
+        part = orc.oracle().render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags, rows=rows,
+                                         threads=1)
+        for i in range(frames):
+            fb = pipe.next_buffer()
+            for f in fb.fields:  # frame i = the rendered frame with steps + i (distinct frames)
+                v = torch.from_numpy(part[f])
+                fb.views[f].copy_(v + i if f == "steps" else v)
+            pipe.submit()
+        img = pipe.finish()
+        if rank == 0:
+            np.savez(out_path, **{f: v.numpy() for f, v in img.items()})
+        else:
+            assert img is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mode,frames", [(2, "shards", 3), (3, "shards", 4),
+                                               (2, "samples", 3), (3, "samples", 1)])
+def test_pipelined_gather(tmp_path, oracle, world, mode, frames):
+    W, H = 16, 24
+    out = str(tmp_path / "frame.npz")
+    mp.spawn(_pipeline_worker, args=(world, _free_port(), mode, W, H, frames, out),
+             nprocs=world, join=True)
+    c, bh, dk, cfg, cam = _scene()
+    with np.load(out) as got:
+        if mode == "shards":
+            want = oracle.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+            for f in abi.SOA_FIELDS:
+                w = want[f] + (frames - 1) if f == "steps" else want[f]
+                assert np.array_equal(got[f].reshape(-1), w, equal_nan=True), f
+            return
+        from bhrt.dist_frame import sample_offset
+        planes = []
+        for k in range(world):
+            cam_k = configs.camera("B")
+            off = sample_offset(k)
+            if off is not None:
+                cam_k.use_offset, cam_k.offset_x, cam_k.offset_y = 1, off[0], off[1]
+            planes.append(oracle.render_frame(bh, dk, cfg, cam_k, W, H, c.method, c.flags))
+        for k, p in enumerate(planes):
+            for f in abi.SOA_FIELDS:
+                w = p[f] + (frames - 1) if f == "steps" else p[f]
+                assert np.array_equal(got[f][k].reshape(-1), w, equal_nan=True), (k, f)
+        mean = np.stack([np.mean([p[ch] for p in planes], axis=0)
+                         for ch in ("rgb_r", "rgb_g", "rgb_b")])
+        np.testing.assert_allclose(got["rgb_mean"].reshape(3, -1), mean, rtol=1e-12)
+        # the offsets really moved the rays
+        assert not np.array_equal(planes[0]["hit_x"], planes[1]["hit_x"], equal_nan=True)

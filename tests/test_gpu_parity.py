@@ -371,3 +371,17 @@ def test_display_path_rgba(bhrt_lib, oracle, cname):
     assert np.array_equal(np.isnan(f32[:, :3]), ~ok)
     np.testing.assert_allclose(f32[:, :3][ok], w32[ok], rtol=1e-5, atol=1e-6)
     assert np.abs(got["rgba8"][:, :3].astype(int) - _display_u8(w32).astype(int)).max() <= 1
+
+
+def test_sub_pixel_offset_frames(bhrt_lib, oracle):
+    """bhrt_camera.use_offset: frames at trace_pixel's jitter offsets (the weak-scaling sample
+    planes of bench.py) against the oracle."""
+    from bhrt.dist_frame import sample_offset
+    c = configs.CONFIGS["C2"]
+    bh, dk, cfg = c.scene()
+    for k in (1, 2, 5):
+        cam = configs.camera("B")
+        cam.use_offset, (cam.offset_x, cam.offset_y) = 1, sample_offset(k)
+        got = bhrt_lib.render_frame(bh, dk, cfg, cam, 64, 36, c.method, c.flags)
+        want = oracle.render_frame(bh, dk, cfg, cam, 64, 36, c.method, c.flags)
+        compare(got, want, RTOL, False, f"sample {k}")
