@@ -39,7 +39,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from bhrt import abi, configs, lib  # noqa: E402
-from bhrt.dist_frame import FramePipeline, sample_offset  # noqa: E402
+from bhrt.dist_frame import FramePipeline, padded_shard_rows, sample_offset  # noqa: E402
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (and FP64 matrix) peak, AMD spec
 METRIC = "Mrays/s (and RK4 steps/s) per GPU + per node; max |Δhit| vs CPU ref"
@@ -91,7 +91,7 @@ def main():
     W, H = c.width, c.bench_height(1)
     if strong:
         rows = abi.Rows(ROW_BLOCK, rank, world) if world > 1 else None
-        n = lib.shard_rows(H, rows) * W
+        n = padded_shard_rows(H, ROW_BLOCK, world) * W  # this rank fills its shard_rows
     else:
         rows = None
         n = W * H

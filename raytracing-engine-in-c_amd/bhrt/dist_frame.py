@@ -35,6 +35,14 @@ def shard_row_count(H, row_block, shard, world):
     return n
 
 
+def padded_shard_rows(H, row_block, world):
+    """Rows of every shard's buffer in "shards" mode: the largest shard, in whole blocks, so
+    all ranks gather equal-sized buffers. A shard's padding rows map to image rows >= H."""
+    if world <= 1:
+        return H
+    return -(-H // (row_block * world)) * row_block
+
+
 def shard_rows_index(H, row_block, shard, world):
     """Image row of each local row of `shard`, in local order."""
     n = shard_row_count(H, row_block, shard, world)
@@ -100,6 +108,8 @@ def sample_offset(k):
 class FramePipeline:
     """Double-buffered render -> gather-to-rank-0 -> assemble.
 
+    n = rays per rank buffer: W * H ("samples"), W * padded_shard_rows(...) ("shards", of
+    which a rank renders its first W * shard_row_count(...)).
     Per frame: fb = next_buffer(); render into fb; submit(). finish() completes the gathers
     still in flight and returns rank 0's newest assembled frame (None elsewhere):
       shards:  {field: [H, W]}
@@ -155,10 +165,11 @@ class FramePipeline:
         if self.mode == "shards":
             if world == 1:
                 return {f: fb.views[f].view(H, W) for f in fb.fields}
-            n_rows, B = fb.n // W, self.row_block
+            n_rows, B = fb.n // W, self.row_block  # padded_shard_rows
             for f in fb.fields:
                 p = torch.stack([fb.view(g, f) for g in parts])  # [world, n_rows*W]
-                img[f] = p.view(world, n_rows // B, B, W).permute(1, 0, 2, 3).reshape(H, W)
+                img[f] = (p.view(world, n_rows // B, B, W).permute(1, 0, 2, 3)
+                          .reshape(world * n_rows, W)[:H])
             return img
         for f in fb.fields:
             img[f] = (fb.views[f].view(1, H, W) if world == 1 else

@@ -111,8 +111,9 @@ def _pipeline_worker(rank, world, port, mode, W, H, frames, out_path):
         c, bh, dk, cfg, cam = _scene()
         B = 4
         if mode == "shards":
+            from bhrt.dist_frame import padded_shard_rows
             rows = abi.Rows(B, rank, world)
-            n = shard_row_count(H, B, rank, world) * W
+            n = padded_shard_rows(H, B, world) * W  # renders shard_row_count(...) rows of it
         else:
             rows, n = None, W * H
             off = sample_offset(rank)
@@ -125,7 +126,7 @@ def _pipeline_worker(rank, world, port, mode, W, H, frames, out_path):
             fb = pipe.next_buffer()
             for f in fb.fields:  # frame i = the rendered frame with steps + i (distinct frames)
                 v = torch.from_numpy(part[f])
-                fb.views[f].copy_(v + i if f == "steps" else v)
+                fb.views[f][:len(v)].copy_(v + i if f == "steps" else v)
             pipe.submit()
         img = pipe.finish()
         if rank == 0:
@@ -136,10 +137,11 @@ def _pipeline_worker(rank, world, port, mode, W, H, frames, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode,frames", [(2, "shards", 3), (3, "shards", 4),
-                                               (2, "samples", 3), (3, "samples", 1)])
-def test_pipelined_gather(tmp_path, oracle, world, mode, frames):
-    W, H = 16, 24
+@pytest.mark.parametrize("world,mode,frames,H", [(2, "shards", 3, 24), (3, "shards", 4, 24),
+                                                 (2, "shards", 2, 20), (3, "shards", 3, 26),
+                                                 (2, "samples", 3, 24), (3, "samples", 1, 24)])
+def test_pipelined_gather(tmp_path, oracle, world, mode, frames, H):
+    W = 16
     out = str(tmp_path / "frame.npz")
     mp.spawn(_pipeline_worker, args=(world, _free_port(), mode, W, H, frames, out),
              nprocs=world, join=True)
