@@ -5,6 +5,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc
+rm -rf $OUT/p[0-9]*   # passes of an earlier run must not mix into this summary
 mkdir -p $OUT
 CFG=${CFG:-C2}
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
