@@ -179,6 +179,14 @@ int calculate_particle_orbit(const ParticleSystem* system, int particle_id,
     return -1;
 }
 
+/* find_particle(system, id) for the id add_particle just returned: ids are unique and the
+ * new particle is the last one, so this is the reference's lookup without its O(count) scan
+ * (which makes creating N particles O(N^2) there). */
+static Particle* just_added(ParticleSystem* system, int id) {
+    Particle* p = &system->particles[system->count - 1];
+    return (p->id == id && p->active) ? p : NULL;
+}
+
 static double urand(void) { return (double)rand() / RAND_MAX; }
 
 int create_accretion_disk(ParticleSystem* system, const BlackHoleParams* bh,
@@ -207,7 +215,7 @@ int create_accretion_disk(ParticleSystem* system, const BlackHoleParams* bh,
         const double temperature = disk->temperature_scale * 10000.0 * pow(inner / r, 0.75);
         const int id = add_particle(system, &pos, &vel, 0.0, PARTICLE_DISK);
         if (id < 0) break;
-        Particle* p = find_particle(system, id);
+        Particle* p = just_added(system, id);
         if (p != NULL) p->temperature = temperature;
         created++;
     }
@@ -235,7 +243,7 @@ int generate_hawking_radiation(ParticleSystem* system, const BlackHoleParams* bh
         vel = vector3D_scale(vector3D_normalize(vel), 1.0 * 0.9);
         const int id = add_particle(system, &pos, &vel, 0.0, PARTICLE_HAWKING);
         if (id < 0) break;
-        Particle* p = find_particle(system, id);
+        Particle* p = just_added(system, id);
         if (p != NULL) p->temperature = hawking_temp;
         created++;
     }
