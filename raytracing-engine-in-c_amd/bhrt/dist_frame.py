@@ -113,7 +113,8 @@ class FramePipeline:
     Per frame: fb = next_buffer(); render into fb; submit(). finish() completes the gathers
     still in flight and returns rank 0's newest assembled frame (None elsewhere):
       shards:  {field: [H, W]}
-      samples: {field: [world, H, W]} plus "rgb_mean" [3, H, W] when rgb was rendered.
+      samples: {field: [world, H, W]} plus, for world > 1, "rgb_mean" [3, H, W] when rgb
+               was rendered (one plane is its own mean).
     """
 
     def __init__(self, n, device, world, rank, mode, H, W, row_block=8,
@@ -174,7 +175,7 @@ class FramePipeline:
         for f in fb.fields:
             img[f] = (fb.views[f].view(1, H, W) if world == 1 else
                       torch.stack([fb.view(g, f) for g in parts]).view(world, H, W))
-        if all(c in img for c in ("rgb_r", "rgb_g", "rgb_b")):
+        if world > 1 and all(c in img for c in ("rgb_r", "rgb_g", "rgb_b")):
             img["rgb_mean"] = torch.stack([img[c].mean(dim=0)
                                            for c in ("rgb_r", "rgb_g", "rgb_b")])
         return img

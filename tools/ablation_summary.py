@@ -24,7 +24,7 @@ for j in sorted(glob.glob(os.path.join(src, "*.json"))):
     rows.append((v, 64 * per.get("SQ_INSTS_VALU", 0) / it,
                  64 * (per.get("SQ_INSTS_VALU_FMA_F64", 0) + per.get("SQ_INSTS_VALU_MUL_F64", 0)
                        + per.get("SQ_INSTS_VALU_ADD_F64", 0)) / it,
-                 b["kernel"]["avg_ms"] * 1e6 / it, it))
+                 b["kernel"]["avg_ms"] * 1e9 / it, it))
 base = {r[0]: r for r in rows}["base"]
 print(f"{'variant':12s} {'VALU/it':>8s} {'dVALU':>7s} {'f64/it':>7s} {'ps/it':>7s} {'iters':>12s}")
 for v, valu, f64, ps, it in rows:
