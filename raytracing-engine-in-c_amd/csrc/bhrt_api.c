@@ -88,6 +88,8 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 #define BHRT_MAX_DEV 16
 #define BHRT_RING 64        /* control blocks per context             */
 #define BHRT_CTL_WORDS 8    /* u64 per control block (64 B)           */
+#define BHRT_MAX_CHUNKS 8   /* host-buffer frames: pipelined chunks per device            */
+#define BHRT_SCRATCH_SLOTS 4
 #define BHRT_NFIELDS 15
 
 typedef struct {
@@ -109,8 +111,18 @@ typedef struct {
     size_t cap_soa; /* rays */
     void* h_stage;  /* pinned staging for SoA readback */
     size_t cap_stage;
-    void* d_init;   /* initial-state table of ray-array launches */
-    size_t cap_init;
+    /* per-stream launch scratch (ray-array init table + redo list), so launches on different
+     * streams never share it; a slot moves to another stream only after its stream drained */
+    struct {
+        hipStream_t stream;
+        void* p;
+        size_t cap;
+    } scratch[BHRT_SCRATCH_SLOTS];
+    int scratch_next;
+    /* host-buffer frames (bhrt_render_frame): two trace streams for overlapping chunks, a
+     * copy stream, and per chunk: trace finished / its D2H landed */
+    hipStream_t stream2, copy;
+    hipEvent_t chunk_done[BHRT_MAX_CHUNKS], chunk_copied[BHRT_MAX_CHUNKS];
 } devctx_t;
 
 static _Thread_local devctx_t* g_ctx[BHRT_MAX_DEV];
@@ -156,9 +168,27 @@ static devctx_t* ctx_get(int device) {
             free(c);
             return NULL;
         }
+    if (hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+        set_err("cannot create the copy stream on device %d", device);
+        free(c);
+        return NULL;
+    }
+    for (int i = 0; i < BHRT_MAX_CHUNKS; i++)
+        if (hipEventCreateWithFlags(&c->chunk_done[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->chunk_copied[i], hipEventDisableTiming) != hipSuccess) {
+            set_err("hipEventCreate failed");
+            free(c);
+            return NULL;
+        }
     g_ctx[device] = c;
     return c;
 }
+
+static int ensure(void** p, size_t* cap, size_t need, int pinned);
+
+/* launch scratch of `stream` on this context, at least `bytes` */
+static void* stream_scratch(devctx_t* c, hipStream_t stream, size_t bytes);
 
 static int ensure(void** p, size_t* cap, size_t need, int pinned) {
     if (*cap >= need && *p) return 0;
@@ -177,6 +207,27 @@ static int ensure(void** p, size_t* cap, size_t need, int pinned) {
     }
     *cap = n;
     return 0;
+}
+
+static void* stream_scratch(devctx_t* c, hipStream_t stream, size_t bytes) {
+    int slot = -1;
+    for (int i = 0; i < BHRT_SCRATCH_SLOTS; i++)
+        if (c->scratch[i].p && c->scratch[i].stream == stream) slot = i;
+    if (slot < 0) {
+        slot = c->scratch_next;
+        c->scratch_next = (c->scratch_next + 1) % BHRT_SCRATCH_SLOTS;
+        if (c->scratch[slot].p && hipStreamSynchronize(c->scratch[slot].stream) != hipSuccess) {
+            set_err("hipStreamSynchronize failed");
+            return NULL;
+        }
+        c->scratch[slot].stream = stream;
+    } else if (c->scratch[slot].cap < bytes &&
+               hipStreamSynchronize(stream) != hipSuccess) { /* in use until drained */
+        set_err("hipStreamSynchronize failed");
+        return NULL;
+    }
+    if (ensure(&c->scratch[slot].p, &c->scratch[slot].cap, bytes ? bytes : 64, 0)) return NULL;
+    return c->scratch[slot].p;
 }
 
 /* fold finished launches into g_stats (waits for them) */
@@ -412,15 +463,16 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
     devctx_t* c = ctx_get(dev);
     if (!c) return -1;
     if (colour_args_bad(out)) return -1;
-    if (ensure(&c->d_init, &c->cap_init,
-               (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) * (size_t)nrows * (size_t)W, 0))
-        return -1;
+    void* scratch = stream_scratch(c, stream ? (hipStream_t)stream : c->stream,
+                                   (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) *
+                                       (size_t)nrows * (size_t)W);
+    if (!scratch) return -1;
     bhrt_kparams kp;
     fill_scene(&kp, bh, dk, cfg, method, flags);
     fill_camera(&kp, cam, W, H);
     if (rows && rows->num_shards > 1) kp.cam.rows = *rows;
     kp.n = nrows * W;
-    kp.init = (double*)c->d_init;
+    kp.init = (double*)scratch;
     kp.out = *out;
     return launch(c, &kp, (hipStream_t)stream);
 }
@@ -436,14 +488,14 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
     if (colour_args_bad(out)) return -1;
     devctx_t* c = ctx_get(current_device());
     if (!c) return -1;
-    if (ensure(&c->d_init, &c->cap_init,
-               (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) * (size_t)n, 0))
-        return -1;
+    void* scratch = stream_scratch(c, stream ? (hipStream_t)stream : c->stream,
+                                   (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) * (size_t)n);
+    if (!scratch) return -1;
     bhrt_kparams kp;
     fill_scene(&kp, bh, dk, cfg, method, flags);
     kp.src = BHRT_SRC_RAYS;
     kp.rays = d_rays;
-    kp.init = (double*)c->d_init;
+    kp.init = (double*)scratch;
     kp.n = n;
     kp.out = *out;
     return launch(c, &kp, (hipStream_t)stream);
@@ -454,10 +506,9 @@ static const size_t k_fsize[BHRT_NFIELDS] = {4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8,
 
 static void** soa_slot(bhrt_frame_soa* s, int f) { return ((void**)s) + f; }
 
-/* carve a device SoA for n rays out of c->d_soa, for the fields `want` requests */
-static int device_soa(devctx_t* c, long n, const bhrt_frame_soa* want_in, bhrt_frame_soa* dev) {
+/* the fields a device SoA needs for the fields `want_in` requests */
+static bhrt_frame_soa device_fields(const bhrt_frame_soa* want_in) {
     bhrt_frame_soa want_buf = *want_in;
-    const bhrt_frame_soa* want = &want_buf;
     if (want_buf.rgb_r || want_buf.rgb_g || want_buf.rgb_b) /* written together */
         want_buf.rgb_r = want_buf.rgb_g = want_buf.rgb_b = (double*)1;
     if (want_buf.rgb_r || want_buf.rgba32f || want_buf.rgba8) { /* the colour pass reads these */
@@ -465,17 +516,33 @@ static int device_soa(devctx_t* c, long n, const bhrt_frame_soa* want_in, bhrt_f
         if (!want_buf.hit_x) want_buf.hit_x = (double*)1;
         if (!want_buf.hit_y) want_buf.hit_y = (double*)1;
     }
+    return want_buf;
+}
+
+static size_t soa_bytes(const bhrt_frame_soa* fields, long n) {
     size_t bytes = 0;
     for (int f = 0; f < BHRT_NFIELDS; f++)
-        if (*soa_slot((bhrt_frame_soa*)want, f)) bytes += ((k_fsize[f] * n + 255) / 256) * 256;
-    if (ensure(&c->d_soa, &c->cap_soa, bytes ? bytes : 256, 0)) return -1;
+        if (*soa_slot((bhrt_frame_soa*)fields, f)) bytes += ((k_fsize[f] * n + 255) / 256) * 256;
+    return bytes;
+}
+
+/* point dev's fields at consecutive 256-byte-aligned arrays of n elements from *p */
+static void soa_carve(char** p, const bhrt_frame_soa* fields, long n, bhrt_frame_soa* dev) {
     memset(dev, 0, sizeof *dev);
-    char* p = (char*)c->d_soa;
     for (int f = 0; f < BHRT_NFIELDS; f++)
-        if (*soa_slot((bhrt_frame_soa*)want, f)) {
-            *soa_slot(dev, f) = p;
-            p += ((k_fsize[f] * n + 255) / 256) * 256;
+        if (*soa_slot((bhrt_frame_soa*)fields, f)) {
+            *soa_slot(dev, f) = *p;
+            *p += ((k_fsize[f] * n + 255) / 256) * 256;
         }
+}
+
+/* carve a device SoA for n rays out of c->d_soa, for the fields `want` requests */
+static int device_soa(devctx_t* c, long n, const bhrt_frame_soa* want_in, bhrt_frame_soa* dev) {
+    const bhrt_frame_soa fields = device_fields(want_in);
+    const size_t bytes = soa_bytes(&fields, n);
+    if (ensure(&c->d_soa, &c->cap_soa, bytes ? bytes : 256, 0)) return -1;
+    char* p = (char*)c->d_soa;
+    soa_carve(&p, &fields, n, dev);
     return 0;
 }
 
@@ -485,35 +552,41 @@ typedef struct {
     long n;
 } shard_job;
 
-/* copy a finished device SoA back into `host` at element offsets given by map(j) */
-static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_rows* rows) {
-    devctx_t* c = j->c;
-    HIP_TRY(hipSetDevice(c->device));
-    /* only the fields the caller asked for (the device may hold extra ones, e.g. the hit
-     * point the colour pass reads) */
-#define WANTED(f) (*soa_slot(&j->dev, f) && *soa_slot((bhrt_frame_soa*)host, f))
+/* only the fields the caller asked for (the device may hold extra ones, e.g. the hit point
+ * the colour pass reads) */
+#define WANTED(j, host, f) \
+    (*soa_slot((bhrt_frame_soa*)&(j)->dev, f) && *soa_slot((bhrt_frame_soa*)(host), f))
+
+static size_t wanted_bytes(const shard_job* j, const bhrt_frame_soa* host) {
     size_t bytes = 0;
     for (int f = 0; f < BHRT_NFIELDS; f++)
-        if (WANTED(f)) bytes += k_fsize[f] * (size_t)j->n;
-    if (ensure(&c->h_stage, &c->cap_stage, bytes ? bytes : 64, 1)) return -1;
-    char* stage = (char*)c->h_stage;
+        if (WANTED(j, host, f)) bytes += k_fsize[f] * (size_t)j->n;
+    return bytes;
+}
+
+/* enqueue the D2H of a shard's wanted fields into pinned `stage` on stream st */
+static int readback_issue(shard_job* j, const bhrt_frame_soa* host, char* stage, hipStream_t st) {
     size_t off = 0;
     for (int f = 0; f < BHRT_NFIELDS; f++) {
-        void* src = *soa_slot(&j->dev, f);
-        if (!WANTED(f)) continue;
-        HIP_TRY(hipMemcpyAsync(stage + off, src, k_fsize[f] * (size_t)j->n,
-                               hipMemcpyDeviceToHost, c->stream));
+        if (!WANTED(j, host, f)) continue;
+        HIP_TRY(hipMemcpyAsync(stage + off, *soa_slot(&j->dev, f), k_fsize[f] * (size_t)j->n,
+                               hipMemcpyDeviceToHost, st));
         off += k_fsize[f] * (size_t)j->n;
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    off = 0;
+    return 0;
+}
+
+/* copy a landed shard from `stage` into `host`, un-permuting cyclic row blocks */
+static void readback_finish(const shard_job* j, const bhrt_frame_soa* host, const char* stage,
+                            int W, const bhrt_rows* rows) {
+    size_t off = 0;
     for (int f = 0; f < BHRT_NFIELDS; f++) {
-        if (!WANTED(f)) continue;
+        if (!WANTED(j, host, f)) continue;
         char* dst = (char*)*soa_slot((bhrt_frame_soa*)host, f);
         size_t fs = k_fsize[f];
         if (!rows || rows->num_shards <= 1) {
             memcpy(dst, stage + off, fs * (size_t)j->n);
-        } else { /* un-permute cyclic row blocks */
+        } else {
             long nrow = j->n / W;
             for (long r = 0; r < nrow; r++) {
                 long B = rows->row_block;
@@ -523,10 +596,25 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
         }
         off += fs * (size_t)j->n;
     }
-#undef WANTED
+}
+
+/* copy a finished device SoA back into `host` (synchronous) */
+static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_rows* rows) {
+    devctx_t* c = j->c;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = wanted_bytes(j, host);
+    if (ensure(&c->h_stage, &c->cap_stage, bytes ? bytes : 64, 1)) return -1;
+    if (readback_issue(j, host, (char*)c->h_stage, c->stream)) return -1;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    readback_finish(j, host, (const char*)c->h_stage, W, rows);
     return 0;
 }
 
+/* Host-buffer frames are traced in K chunks per device -- cyclic row-block shards k*ndev + d
+ * of K*ndev, so every chunk carries the same mix of work -- alternating between two trace
+ * streams, so a chunk's workgroups fill the CUs its predecessor's tail (the longest rays)
+ * frees. A copy stream moves each finished chunk into pinned staging while later ones trace,
+ * and the host un-permutes a chunk into the caller's arrays as soon as it lands. */
 int bhrt_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* dk,
                       const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
                       IntegrationMethod method, int flags, const bhrt_frame_soa* host) {
@@ -539,26 +627,65 @@ int bhrt_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* dk,
         set_err("no HIP device available (libbhrt has no CPU path)");
         return -1;
     }
-    int block = 8;
+    const int block = 8;
     if (ndev > 1 && H < ndev * block) ndev = 1;
-    shard_job jobs[BHRT_MAX_DEV];
-    bhrt_rows rows[BHRT_MAX_DEV];
-    for (int d = 0; d < ndev; d++) {
-        rows[d].row_block = block;
-        rows[d].shard = d;
-        rows[d].num_shards = ndev;
+    const long per_dev = (long)W * H / ndev;  /* chunks per device: */
+    int K = per_dev >= (1L << 21) ? 8 : (per_dev >= (1L << 18) ? 4 : 1);
+    if (H < K * ndev * block) K = 1;
+    const char* env = getenv("BHRT_HOST_CHUNKS");
+    if (env && atoi(env) >= 1 && atoi(env) <= BHRT_MAX_CHUNKS && H >= atoi(env) * ndev * block)
+        K = atoi(env);
+    const int shards = K * ndev;
+    shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
+    bhrt_rows rows[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
+    size_t stage_off[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
+    const bhrt_frame_soa fields = device_fields(host);
+    for (int d = 0; d < ndev; d++) { /* buffers: every chunk of device d */
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
         HIP_TRY(hipSetDevice(d));
-        jobs[d].c = c;
-        jobs[d].n = (long)bhrt_shard_rows(H, &rows[d]) * W;
-        if (device_soa(c, jobs[d].n, host, &jobs[d].dev)) return -1;
-        if (bhrt_render_frame_device(bh, dk, cfg, cam, W, H, &rows[d], method, flags,
-                                     &jobs[d].dev, c->stream))
-            return -1;
+        size_t dev_bytes = 0, host_bytes = 0;
+        for (int k = 0; k < K; k++) {
+            bhrt_rows* r = &rows[k][d];
+            r->row_block = block;
+            r->shard = k * ndev + d;
+            r->num_shards = shards;
+            jobs[k][d].c = c;
+            jobs[k][d].n = shards > 1 ? (long)bhrt_shard_rows(H, r) * W : (long)W * H;
+            dev_bytes += soa_bytes(&fields, jobs[k][d].n);
+        }
+        if (ensure(&c->d_soa, &c->cap_soa, dev_bytes ? dev_bytes : 256, 0)) return -1;
+        char* p = (char*)c->d_soa;
+        for (int k = 0; k < K; k++) {
+            soa_carve(&p, &fields, jobs[k][d].n, &jobs[k][d].dev);
+            stage_off[k][d] = host_bytes;
+            host_bytes += wanted_bytes(&jobs[k][d], host);
+        }
+        if (ensure(&c->h_stage, &c->cap_stage, host_bytes ? host_bytes : 64, 1)) return -1;
     }
-    for (int d = 0; d < ndev; d++)
-        if (readback(&jobs[d], host, W, ndev > 1 ? &rows[d] : NULL)) return -1;
+    for (int k = 0; k < K; k++) /* trace, then queue each chunk's copy behind it */
+        for (int d = 0; d < ndev; d++) {
+            devctx_t* c = jobs[k][d].c;
+            hipStream_t st = (k & 1) ? c->stream2 : c->stream;
+            HIP_TRY(hipSetDevice(d));
+            if (jobs[k][d].n > 0 &&
+                bhrt_render_frame_device(bh, dk, cfg, cam, W, H, shards > 1 ? &rows[k][d] : NULL,
+                                         method, flags, &jobs[k][d].dev, st))
+                return -1;
+            HIP_TRY(hipEventRecord(c->chunk_done[k], st));
+            HIP_TRY(hipStreamWaitEvent(c->copy, c->chunk_done[k], 0));
+            if (readback_issue(&jobs[k][d], host, (char*)c->h_stage + stage_off[k][d], c->copy))
+                return -1;
+            HIP_TRY(hipEventRecord(c->chunk_copied[k], c->copy));
+        }
+    for (int k = 0; k < K; k++) /* un-permute each chunk as it lands */
+        for (int d = 0; d < ndev; d++) {
+            devctx_t* c = jobs[k][d].c;
+            HIP_TRY(hipSetDevice(d));
+            HIP_TRY(hipEventSynchronize(c->chunk_copied[k]));
+            readback_finish(&jobs[k][d], host, (const char*)c->h_stage + stage_off[k][d], W,
+                            shards > 1 ? &rows[k][d] : NULL);
+        }
     return 0;
 }
 

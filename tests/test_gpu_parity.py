@@ -385,3 +385,24 @@ def test_sub_pixel_offset_frames(bhrt_lib, oracle):
         got = bhrt_lib.render_frame(bh, dk, cfg, cam, 64, 36, c.method, c.flags)
         want = oracle.render_frame(bh, dk, cfg, cam, 64, 36, c.method, c.flags)
         compare(got, want, RTOL, False, f"sample {k}")
+
+
+def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch):
+    """bhrt_render_frame traces a host-buffer frame in pipelined chunks (cyclic row-block
+    shards, copies overlapped with tracing); any chunk count gives the device frame."""
+    import torch
+    c = configs.CONFIGS["C2"]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera("B")
+    W, H = 640, 416
+    t = {f: torch.zeros(W * H, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
+                        device="cuda") for f in abi.SOA_FIELDS}
+    bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                 bhrt_lib.soa_from_tensors(t), 0)
+    torch.cuda.synchronize()
+    ref = {f: v.cpu().numpy() for f, v in t.items()}
+    for chunks in ("1", "3", "4", "8"):
+        monkeypatch.setenv("BHRT_HOST_CHUNKS", chunks)
+        got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+        for f in abi.SOA_FIELDS:
+            assert np.array_equal(got[f], ref[f], equal_nan=True), (chunks, f)
