@@ -111,6 +111,8 @@ typedef struct {
     size_t cap_soa; /* rays */
     void* h_stage;  /* pinned staging for SoA readback */
     size_t cap_stage;
+    void* h_rays;   /* pinned staging for ray uploads (trace_rays_batch) */
+    size_t cap_hrays;
     /* per-stream launch scratch (ray-array init table + redo list), so launches on different
      * streams never share it; a slot moves to another stream only after its stream drained */
     struct {
@@ -738,45 +740,124 @@ int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
 
 /* trace rays into RayTraceHit[], writing exactly the fields trace_ray writes
  * (raytracer.c:299-333, 728-753) */
+/* pack one traced range into the reference's RayTraceHit (fill_hit_info, raytracer.c:299-333,
+ * and trace_ray's disk branch :728-753): only the fields the reference writes */
+static void pack_hits(RayTraceHit* hits, long n, const bhrt_frame_soa* s, int nthreads) {
+#pragma omp parallel for schedule(static) num_threads(nthreads) if (n >= 65536)
+    for (long i = 0; i < n; i++) {
+        RayTraceHit* h = &hits[i];
+        h->result = (RayTraceResult)s->result[i];
+        h->steps = s->steps[i];
+        h->hit_position.x = s->hit_x[i];
+        h->hit_position.y = s->hit_y[i];
+        h->hit_position.z = s->hit_z[i];
+        h->distance = s->distance[i];
+        h->time_dilation = s->time_dilation[i];
+        if (h->result == RAY_MAX_DISTANCE) {
+            h->sky_direction.x = s->sky_x[i];
+            h->sky_direction.y = s->sky_y[i];
+            h->sky_direction.z = s->sky_z[i];
+        }
+    }
+}
+
+/* the SoA fields a RayTraceHit needs, laid out consecutively from p for n rays */
+static void hit_fields(char* p, long n, bhrt_frame_soa* s) {
+    memset(s, 0, sizeof *s);
+    s->result = (int32_t*)p;
+    s->steps = s->result + n;
+    s->hit_x = (double*)(s->steps + n);
+    s->hit_y = s->hit_x + n;
+    s->hit_z = s->hit_y + n;
+    s->distance = s->hit_z + n;
+    s->time_dilation = s->distance + n;
+    s->sky_x = s->time_dilation + n;
+    s->sky_y = s->sky_x + n;
+    s->sky_z = s->sky_y + n;
+}
+#define HIT_BYTES (2 * sizeof(int32_t) + 8 * sizeof(double))
+
+/* Large batches: K contiguous chunks per device on alternating trace streams. Launching chunk
+ * k first copies its rays into pinned staging (so the upload is asynchronous and overlaps the
+ * chunks already tracing); each chunk's results come back on the copy stream, and the host
+ * packs a chunk into hits[] as soon as it lands, with nthreads threads. */
+static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* bh,
+                                const AccretionDiskParams* dk, const SimulationConfig* cfg,
+                                RayTraceHit* hits, int nthreads) {
+    int ndev = bhrt_device_count();
+    if (ndev <= 0) {
+        set_err("no HIP device available (libbhrt has no CPU path)");
+        return -1;
+    }
+    const int K = (long)n / ndev >= (1L << 20) ? 8 : 4;
+    long base[BHRT_MAX_CHUNKS + 1][BHRT_MAX_DEV]; /* chunk k of device d: [base[k][d], base[k+1][d]) */
+    shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
+    for (int d = 0; d < ndev; d++) {
+        const long d0 = (long)n * d / ndev, d1 = (long)n * (d + 1) / ndev;
+        for (int k = 0; k <= K; k++) base[k][d] = d0 + (d1 - d0) * k / K;
+        devctx_t* c = ctx_get(d);
+        if (!c) return -1;
+        HIP_TRY(hipSetDevice(d));
+        const long m = d1 - d0;
+        if (ensure(&c->d_rays, &c->cap_rays, (size_t)m * sizeof(Ray), 0) ||
+            ensure(&c->d_soa, &c->cap_soa, (size_t)m * HIT_BYTES + 4096 * K, 0) ||
+            ensure(&c->h_rays, &c->cap_hrays, (size_t)m * sizeof(Ray), 1) ||
+            ensure(&c->h_stage, &c->cap_stage, (size_t)m * HIT_BYTES, 1))
+            return -1;
+    }
+    for (int k = 0; k < K; k++)
+        for (int d = 0; d < ndev; d++) {
+            devctx_t* c = ctx_get(d);
+            hipStream_t st = (k & 1) ? c->stream2 : c->stream;
+            HIP_TRY(hipSetDevice(d));
+            const long d0 = base[0][d], a = base[k][d] - d0, m = base[k + 1][d] - base[k][d];
+            jobs[k][d].c = c;
+            jobs[k][d].n = m;
+            hit_fields((char*)c->d_soa + (size_t)a * HIT_BYTES + 256 * k, m, &jobs[k][d].dev);
+            if (m > 0) {
+                Ray* hr = (Ray*)c->h_rays + a;
+                memcpy(hr, rays + base[k][d], (size_t)m * sizeof(Ray));
+                HIP_TRY(hipMemcpyAsync((Ray*)c->d_rays + a, hr, (size_t)m * sizeof(Ray),
+                                       hipMemcpyHostToDevice, st));
+                if (bhrt_trace_rays_device((const Ray*)c->d_rays + a, (int)m, bh, dk, cfg,
+                                           INTEGRATOR_RK4, 0, &jobs[k][d].dev, st))
+                    return -1;
+            }
+            HIP_TRY(hipEventRecord(c->chunk_done[k], st));
+            HIP_TRY(hipStreamWaitEvent(c->copy, c->chunk_done[k], 0));
+            if (m > 0) /* device and staging chunks share hit_fields' layout: one copy */
+                HIP_TRY(hipMemcpyAsync((char*)c->h_stage + (size_t)a * HIT_BYTES,
+                                       jobs[k][d].dev.result, (size_t)m * HIT_BYTES,
+                                       hipMemcpyDeviceToHost, c->copy));
+            HIP_TRY(hipEventRecord(c->chunk_copied[k], c->copy));
+        }
+    for (int k = 0; k < K; k++)
+        for (int d = 0; d < ndev; d++) {
+            devctx_t* c = jobs[k][d].c;
+            const long a = base[k][d] - base[0][d], m = jobs[k][d].n;
+            HIP_TRY(hipSetDevice(d));
+            HIP_TRY(hipEventSynchronize(c->chunk_copied[k]));
+            bhrt_frame_soa s;
+            hit_fields((char*)c->h_stage + (size_t)a * HIT_BYTES, m, &s);
+            pack_hits(hits + base[k][d], m, &s, nthreads);
+        }
+    return 0;
+}
+
 static int trace_into_hits(const Ray* rays, int n, const BlackHoleParams* bh,
                            const AccretionDiskParams* dk, const SimulationConfig* cfg,
-                           RayTraceHit* hits) {
-    size_t per = 2 * sizeof(int32_t) + 8 * sizeof(double);
-    char* buf = (char*)malloc(per * (size_t)n);
+                           RayTraceHit* hits, int nthreads) {
+    if (nthreads <= 0) nthreads = 8;
+    if (n >= (1 << 16)) return trace_hits_pipelined(rays, n, bh, dk, cfg, hits, nthreads);
+    char* buf = (char*)malloc(HIT_BYTES * (size_t)n);
     if (!buf) {
         set_err("host allocation failed");
         return -1;
     }
     bhrt_frame_soa s;
-    memset(&s, 0, sizeof s);
-    s.result = (int32_t*)buf;
-    s.steps = s.result + n;
-    s.hit_x = (double*)(s.steps + n);
-    s.hit_y = s.hit_x + n;
-    s.hit_z = s.hit_y + n;
-    s.distance = s.hit_z + n;
-    s.time_dilation = s.distance + n;
-    s.sky_x = s.time_dilation + n;
-    s.sky_y = s.sky_x + n;
-    s.sky_z = s.sky_y + n;
+    hit_fields(buf, n, &s);
     int rc = bhrt_trace_rays(rays, n, bh, dk, cfg, INTEGRATOR_RK4, 0, &s);
-    if (rc == 0) {
-        for (int i = 0; i < n; i++) {
-            RayTraceHit* h = &hits[i];
-            h->result = (RayTraceResult)s.result[i];
-            h->steps = s.steps[i];
-            h->hit_position.x = s.hit_x[i];
-            h->hit_position.y = s.hit_y[i];
-            h->hit_position.z = s.hit_z[i];
-            h->distance = s.distance[i];
-            h->time_dilation = s.time_dilation[i];
-            if (h->result == RAY_MAX_DISTANCE) {
-                h->sky_direction.x = s.sky_x[i];
-                h->sky_direction.y = s.sky_y[i];
-                h->sky_direction.z = s.sky_z[i];
-            }
-        }
-    }
+    if (rc == 0) pack_hits(hits, n, &s, 1);
     free(buf);
     return rc;
 }
@@ -787,7 +868,7 @@ RayTraceResult trace_ray(const Ray* ray, const BlackHoleParams* bh,
     if (!ray || check_scene(bh, cfg)) return RAY_ERROR;
     RayTraceHit tmp;
     RayTraceHit* h = hit ? hit : &tmp;
-    if (trace_into_hits(ray, 1, bh, dk, cfg, h) != 0) {
+    if (trace_into_hits(ray, 1, bh, dk, cfg, h, 1) != 0) {
         if (hit) hit->result = RAY_ERROR;
         return RAY_ERROR;
     }
@@ -797,13 +878,14 @@ RayTraceResult trace_ray(const Ray* ray, const BlackHoleParams* bh,
 int trace_rays_batch(const Ray* rays, int n, const BlackHoleParams* bh,
                      const AccretionDiskParams* dk, const SimulationConfig* cfg,
                      RayTraceHit* hits, int num_threads) {
-    (void)num_threads;
     if (!rays || !bh || !hits || n <= 0) return -1; /* raytracer.c:791-793 */
     if (!cfg) {
         set_err("config must not be NULL");
         return -1;
     }
-    if (trace_into_hits(rays, n, bh, dk, cfg, hits) != 0) {
+    /* num_threads: the reference's OpenMP thread count; here the host threads that pack the
+     * results into hits[] (0 = 8) */
+    if (trace_into_hits(rays, n, bh, dk, cfg, hits, num_threads) != 0) {
         for (int i = 0; i < n; i++) hits[i].result = RAY_ERROR;
         return -1;
     }

@@ -406,3 +406,31 @@ def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch):
         got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
         for f in abi.SOA_FIELDS:
             assert np.array_equal(got[f], ref[f], equal_nan=True), (chunks, f)
+
+
+@pytest.mark.parametrize("n", [65536, 300_001, (1 << 20) + 7])  # 4, 4 and 8 chunks
+def test_large_batch_pipelined_equals_soa_trace(bhrt_lib, n):
+    """trace_rays_batch at n >= 65536 takes the chunked path (rays staged through pinned
+    memory, chunks on two trace streams, results packed into RayTraceHit[] by OpenMP
+    threads): every hit must equal the one-shot SoA trace of the same rays, and sky_direction
+    must stay untouched for rays that did not escape (raytracer.c:299-333)."""
+    rng = np.random.default_rng(n)
+    bh, dk, cfg = configs.CONFIGS["C2"].scene()
+    rays = np.zeros(n, dtype=abi.RAY_DTYPE)
+    rays["origin"] = (0.0, 2.0, -30.0)
+    d = rng.normal(size=(n, 3)) * (0.25, 0.25, 1.0) + (0.0, 0.0, 1.0)
+    rays["direction"] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    ref = bhrt_lib.trace_rays(rays, bh, dk, cfg)
+    rc, hits = bhrt_lib.trace_rays_batch(rays, bh, dk, cfg)
+    assert rc == 0
+    assert np.array_equal(hits["result"], ref["result"])
+    assert np.array_equal(hits["steps"], ref["steps"])
+    for i, ax in enumerate("xyz"):
+        assert np.array_equal(hits["hit_position"][:, i], ref["hit_" + ax], equal_nan=True)
+    assert np.array_equal(hits["distance"], ref["distance"], equal_nan=True)
+    assert np.array_equal(hits["time_dilation"], ref["time_dilation"], equal_nan=True)
+    esc = hits["result"] == abi.RAY_MAX_DISTANCE
+    assert esc.any() and (~esc).any()
+    for i, ax in enumerate("xyz"):
+        assert np.array_equal(hits["sky_direction"][esc, i], ref["sky_" + ax][esc])
+    assert not hits["sky_direction"][~esc].any()
