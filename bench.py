@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--cpu-rows-stride", type=int, default=27,
                    help="CPU baseline samples every k-th image row")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-path", action="store_true",
+                   help="skip the host-buffer leg (its chunked launches would mix into a "
+                        "profiler's per-launch kernel averages)")
     p.add_argument("--sample", type=int, default=None,
                    help="weak scaling: trace sample plane K instead of this rank's (to time "
                         "each plane of an N-GPU run on one GPU)")
@@ -189,7 +192,7 @@ def main():
             "traffic": traffic_from_profile(args.config),
         },
     }
-    if world == 1:
+    if world == 1 and not args.no_host_path:
         out["host_path"] = host_path_rate(c, bh, dk, cfg, cam, W, H)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["max_rel_dhit"], out["class_mismatch"] = cpu_baseline(

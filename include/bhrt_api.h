@@ -305,7 +305,7 @@ int bhrt_get_stats(bhrt_stats* out, int reset);
 int bhrt_device_count(void);
 
 /* Tuning knob: refill a wavefront's finished lanes once at least this many are idle
- * (1..64, default 8). Affects speed only. */
+ * (1..64; 0 = per scene: 8 for RK4 at spin 0, else 64). Affects speed only. */
 void bhrt_set_refill_threshold(int lanes);
 
 /* update_particles (particle_sim.c:505-566) applied `steps` times in one device round trip:

@@ -129,10 +129,18 @@ typedef struct {
 
 static _Thread_local devctx_t* g_ctx[BHRT_MAX_DEV];
 static _Thread_local bhrt_stats g_stats;
-static int g_refill = 8;
+static int g_refill = 0; /* 0: chosen per scene (refill_default) */
 
 void bhrt_set_refill_threshold(int lanes) {
-    g_refill = lanes < 1 ? 1 : (lanes > 64 ? 64 : lanes);
+    g_refill = lanes <= 0 ? 0 : (lanes > 64 ? 64 : lanes);
+}
+
+/* Refill threshold by the expected ray lifetime. RK4 on a = 0: lifetimes
+ * spread over 1..max_steps iterations (C2), so idle lanes are refilled early (8). Otherwise
+ * (Kerr: straight-line stages; RKF45: fixed point after a few attempts) rays are short-lived
+ * and similar, each refill is an HBM-latency stall, and a wave refills only once drained. */
+static int refill_default(const bhrt_scene_k* s) {
+    return (s->method == INTEGRATOR_RK4 && s->spin0) ? 8 : 64;
 }
 
 int bhrt_device_count(void) {
@@ -324,7 +332,7 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
         s->disk_in_sq = sqrt_lower_bound(dk->inner_radius);
         s->disk_out_sq = sqrt_upper_bound(dk->outer_radius);
     }
-    kp->refill = g_refill;
+    kp->refill = g_refill ? g_refill : refill_default(s);
     kp->cam.rows.row_block = 1;
     kp->cam.rows.num_shards = 1;
     return 0;

@@ -54,12 +54,15 @@ struct Counters {
     bool huge = false;  // a sincos argument needed the large-argument path (see bhrt_sincos)
 };
 
-// IEEE-exact division without the generic fdiv scaffolding.
+// Division without the generic fdiv scaffolding.
 // rcp_nr is the reciprocal refinement the compiler's f64 fdiv performs after v_div_scale
-// (v_rcp_f64 + two Newton steps); div_nr is its quotient step (q = a*y, one FMA residual,
-// one FMA correction). For operands in the normal range v_div_scale is the identity, so
-// div_nr(a, b, rcp_nr(b)) is bit-identical to a / b -- and one reciprocal serves every
-// quotient with the same divisor. Callers keep the IEEE a / b for out-of-range operands.
+// (v_rcp_f64 + two Newton steps): RN(1/b) for b in the normal range, and one reciprocal
+// serves every quotient with the same divisor. div_nr(a, b, rcp_nr(b)) is a * RN(1/b)
+// (<= 1.5 ulp; the same order as the FMA contraction of BHRT_CONTRACT): on every BASELINE
+// config it leaves the class and step of every sampled ray equal to the compiled reference's
+// and the hit points as close (profiles/r01_bench_all_configs_v6.jsonl), for 7% of C2.
+// BHRT_EXACT_DIV=1 adds the quotient's residual correction, which makes it bit-identical
+// to a / b (the A/B build "exdiv"). Callers keep the IEEE a / b for out-of-range operands.
 __device__ __forceinline__ double rcp_nr(double b) {
     double y = __builtin_amdgcn_rcp(b);
     double e = __builtin_fma(-b, y, 1.0);
@@ -67,9 +70,17 @@ __device__ __forceinline__ double rcp_nr(double b) {
     e = __builtin_fma(-b, y, 1.0);
     return __builtin_fma(y, e, y);
 }
+#ifndef BHRT_EXACT_DIV
+#define BHRT_EXACT_DIV 0
+#endif
 __device__ __forceinline__ double div_nr(double a, double b, double yb) {
     const double q = a * yb;
+#if BHRT_EXACT_DIV
     return __builtin_fma(__builtin_fma(-b, q, a), yb, q);
+#else
+    (void)b;
+    return q;
+#endif
 }
 // a / 6.0, correctly rounded: RN(1/6) is the exact reciprocal's rounding (Markstein).
 __device__ __forceinline__ double div6(double a) {
@@ -207,6 +218,9 @@ struct Trig1 {
 #ifndef BHRT_LAZY_CLAMP
 #define BHRT_LAZY_CLAMP 1
 #endif
+#ifndef BHRT_TEST_D012
+#define BHRT_TEST_D012 0
+#endif
 template <bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const Scene& sc,
                                     bool far_ok, Counters& n, Trig1& tr, bool first) {
@@ -278,9 +292,14 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
 #if BHRT_LAZY_CLAMP
     // Neither ever applies on a C2 frame (none of 8.3e7 evaluations): one test
     // per component (NaN and Inf fail |d| <= 10) sends the rare lane through the literal repair.
-    const int plain = (int)(fabs(d[3]) <= 10.0) & (int)(fabs(d[4]) <= 10.0) &
-                      (int)(fabs(d[5]) <= 10.0) & (int)isfinite(d[0]) & (int)isfinite(d[1]) &
-                      (int)isfinite(d[2]);
+    // d[0..2] = y[3..5] need no test: the iteration starts from a finite state (ray_iterate's
+    // loop-top repair), and a stage state's y[3..5] is that state plus h * (coefficients of
+    // |.| <= 8) * k[3..5], which this clamp bounds by 10 -- finite.
+    int plain = (int)(fabs(d[3]) <= 10.0) & (int)(fabs(d[4]) <= 10.0) &
+                (int)(fabs(d[5]) <= 10.0);
+#if BHRT_TEST_D012
+    plain &= (int)isfinite(d[0]) & (int)isfinite(d[1]) & (int)isfinite(d[2]);
+#endif
     if (plain) return;
 #endif
 #pragma unroll

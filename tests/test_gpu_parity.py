@@ -237,17 +237,18 @@ def test_device_api_on_torch_stream(bhrt_lib):
     assert counts.sum().item() == W * H
 
 
-def test_refill_threshold_does_not_change_results(bhrt_lib):
-    """The wave refill policy is a speed knob only."""
+@pytest.mark.parametrize("cname", ["C2", "C4", "C5"])
+def test_refill_threshold_does_not_change_results(bhrt_lib, cname):
+    """The wave refill policy (0 = the per-scene default) is a speed knob only."""
     L = bhrt_lib.load()
-    c = configs.CONFIGS["C2"]
+    c = configs.CONFIGS[cname]
     bh, dk, cfg = c.scene()
     cam = configs.camera("B")
     outs = []
-    for thr in (1, 8, 64):
+    for thr in (0, 1, 8, 64):
         L.bhrt_set_refill_threshold(thr)
         outs.append(bhrt_lib.render_frame(bh, dk, cfg, cam, 200, 120, c.method, c.flags))
-    L.bhrt_set_refill_threshold(8)
+    L.bhrt_set_refill_threshold(0)
     for o in outs[1:]:
         for f in abi.SOA_FIELDS:
             assert np.array_equal(o[f], outs[0][f], equal_nan=True), f

@@ -1,7 +1,7 @@
 #!/bin/bash
 # bench.py over every BASELINE configuration at N=1 (C1..C5); one JSON line each.
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/bench_all; mkdir -p $OUT
+OUT=${OUT:-gpurun_out/bench_all}; mkdir -p $OUT
 for c in ${CONFIGS:-C1 C2 C3 C4 C5}; do
   timeout -k 10 600 python bench.py --config $c --steps ${STEPS:-3} --warmup 1 > $OUT/$c.json 2> $OUT/$c.err \
     || { echo "$c failed"; tail -5 $OUT/$c.err; exit 1; }
