@@ -36,6 +36,10 @@
 #ifndef BHRT_FAST_SINCOS
 #define BHRT_FAST_SINCOS 1
 #endif
+#ifndef BHRT_STATS
+#define BHRT_STATS 0
+#endif
+#define BHRT_STATS_N 64
 #if BHRT_CONTRACT
 #pragma clang fp contract(fast)
 #else
@@ -52,7 +56,31 @@ using Scene = bhrt_scene_k;
 struct Counters {
     unsigned rays = 0, iters = 0, full = 0, far_ = 0, kerr = 0;
     bool huge = false;  // a sincos argument needed the large-argument path (see bhrt_sincos)
+#if BHRT_STATS
+    unsigned ds[BHRT_STATS_N] = {};  // instrumented build only (tools/delta_stats.py)
+#endif
 };
+
+#if BHRT_STATS
+// Diagnostic build (make stats): per shift site (0..2 RK stages 2..4, 3..5 the carried
+// advances of y1, y2, y3) lanes and waves whose |delta| exceeds 0.05 / 0.1 / 0.2 / pi/4,
+// plus lane occupancy of the persistent loop. Never part of the product build.
+__device__ unsigned long long g_dstats[BHRT_STATS_N];
+__device__ __forceinline__ void dstat(Counters& n, int site, double delta) {
+    const double thr[4] = {0.05, 0.1, 0.2, 0.78539816339744828};
+    const unsigned long long act = __ballot(1);
+    const bool leader = (threadIdx.x & 63) == __ffsll((long long)act) - 1;
+    unsigned* c = n.ds + site * 10;
+    c[0]++;
+    if (leader) c[1]++;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const bool big = !(fabs(delta) <= thr[j]);
+        if (big) c[2 + j]++;
+        if (__ballot(big) && leader) c[6 + j]++;
+    }
+}
+#endif
 
 // Division without the generic fdiv scaffolding.
 // rcp_nr is the reciprocal refinement the compiler's f64 fdiv performs after v_div_scale
@@ -83,7 +111,7 @@ __device__ __forceinline__ double div_nr(double a, double b, double yb) {
 #endif
 }
 // a / 6.0, correctly rounded: RN(1/6) is the exact reciprocal's rounding (Markstein).
-__device__ __forceinline__ double div6(double a) {
+__device__ __forceinline__ __attribute__((unused)) double div6(double a) {
     constexpr double y = 1.0 / 6.0;
     const double q = a * y;
     return __builtin_fma(__builtin_fma(-6.0, q, a), y, q);
@@ -182,8 +210,8 @@ __device__ __forceinline__ void bhrt_sincos(double x, double* so, double* co,
 // (error <= the direct value's + 0.5 ulp). Returns false, leaving the outputs unset, when
 // delta is outside [-pi/4, pi/4] or when a + delta - a would not be exact; the caller then
 // evaluates sincos directly.
-__device__ __forceinline__ bool sincos_shift(double a, double s0, double c0, double x, double& s,
-                                             double& c) {
+__device__ __forceinline__ bool sincos_shift_wide(double a, double s0, double c0, double x,
+                                                  double& s, double& c) {
     const double delta = x - a;  // exact when x in [a/2, 2a] (Sterbenz)
     if (!(fabs(delta) <= 0.78539816339744828 && fabs(delta) <= 0.5 * fabs(a))) return false;
     constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
@@ -203,6 +231,37 @@ __device__ __forceinline__ bool sincos_shift(double a, double s0, double c0, dou
     return true;
 }
 
+// sin, cos of x given those of a nearby a, as the trace loop needs them. Nearly every shift is
+// tiny (on a full C2 frame |x - a| > 0.0625 in < 0.7% of wave evaluations at any site,
+// tools/delta_stats.py), so every lane first runs polynomials fitted to |delta| <= 1/16 --
+// three coefficients each for sin(delta) and cos(delta) - 1 instead of fdlibm's six, max error
+// 2.4e-19 / 1.0e-21 (tools/shift_poly_fit.py) -- straight-line, and only a lane outside that
+// interval then redoes the shift with sincos_shift_wide (|delta| <= pi/4) or evaluates directly.
+// The choice is per lane, so a ray's rounding never depends on its wave-mates.
+#ifndef BHRT_SHORT_SHIFT
+#define BHRT_SHORT_SHIFT 1
+#endif
+__device__ __forceinline__ void shift_or_eval(double a, double s0, double c0, double x, double& s,
+                                              double& c, Counters* hc) {
+#if BHRT_SHORT_SHIFT
+    const double delta = x - a;  // exact when |delta| <= |a| / 2 (Sterbenz)
+    constexpr double S1 = -0.16666666666662605, S2 = 0.00833333327878775,
+                     S3 = -0.00019839069723619096;
+    constexpr double C1 = 0.04166666666666157, C2 = -0.0013888888827212717,
+                     C3 = 2.479927034006378e-05;
+    const double z = delta * delta;
+    const double sd = delta + (z * delta) * fmac_k(z, fmac_k(z, S3, S2), S1);  // sin(delta)
+    const double cm1 = z * __builtin_fma(z, fmac_k(z, fmac_k(z, C3, C2), C1), -0.5);
+    s = s0 + (s0 * cm1 + c0 * sd);
+    c = c0 + (c0 * cm1 - s0 * sd);
+    if (__builtin_expect(!(fabs(delta) <= 0.0625 && fabs(delta) <= 0.5 * fabs(a)), 0)) {
+        if (!sincos_shift_wide(a, s0, c0, x, s, c)) bhrt_sincos(x, &s, &c, hc);
+    }
+#else
+    if (!sincos_shift_wide(a, s0, c0, x, s, c)) bhrt_sincos(x, &s, &c, hc);
+#endif
+}
+
 // ray_derivatives (raytracer.c:44-154). y = (t, r, theta, phi, tdot, rdot) of the caller,
 // read -- as the reference does -- as (r, theta, phi, v_r, v_theta, v_phi).
 // Trig of theta (= y[1]) for one RK stage: stage 1 evaluates it (or, with BHRT_TRIG_CHAIN,
@@ -212,11 +271,20 @@ __device__ __forceinline__ bool sincos_shift(double a, double s0, double c0, dou
 #endif
 struct Trig1 {
     double a = __builtin_nan(""), s = 0.0, c = 0.0;  // theta of stage 1 and its sin, cos;
+#if BHRT_STATS
+    int site = 0;
+#endif
 };                                                   // NaN until stage 1 evaluated them
 
 // HUGE: keep the large-argument sincos path (else flag it, see bhrt_sincos)
 #ifndef BHRT_LAZY_CLAMP
 #define BHRT_LAZY_CLAMP 1
+#endif
+#ifndef BHRT_FOLD_SIXTH
+#define BHRT_FOLD_SIXTH 1
+#endif
+#ifndef BHRT_FOLD_TERM1
+#define BHRT_FOLD_TERM1 1
 #endif
 #ifndef BHRT_TEST_D012
 #define BHRT_TEST_D012 0
@@ -248,8 +316,11 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
             tr.s = st;
             tr.c = ct;
 #endif
-        } else if (!sincos_shift(tr.a, tr.s, tr.c, y[1], st, ct)) {
-            bhrt_sincos(y[1], &st, &ct, HUGE ? nullptr : &n);
+        } else {
+#if BHRT_STATS
+            dstat(n, tr.site++, y[1] - tr.a);
+#endif
+            shift_or_eval(tr.a, tr.s, tr.c, y[1], st, ct, HUGE ? nullptr : &n);
         }
         double st2 = st * st;
         if (r <= sc.rs_x1_5) {
@@ -268,9 +339,14 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         const double sc4 = st * ct * y[5] * y[5];
         if (r < 1.0e150) {  // r >= 1.5 rs here: every divisor is in the normal range
             const double yr = rcp_nr(r);
+#if BHRT_FOLD_TERM1
+            // -M / (r^2 f) * f == -M / r^2 in exact arithmetic (A/B variant "fold")
+            const double term1 = -(sc.M * yr) * yr;
+#else
             const double f = 1.0 - div_nr(sc.rs, r, yr);
             const double den = rsq * f;
             const double term1 = -div_nr(sc.M, den, rcp_nr(den)) * f;
+#endif
             d[3] = term1 + term2 + term3;
             d[4] = div_nr(n4, r, yr) + sc4;
             d[5] = div_nr(n5a, r, yr) - div_nr(n5b, st, rcp_nr(st));
@@ -316,6 +392,9 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
                                          Counters& n, Trig1& tr) {
     double k[6], acc[6], yt[6];
     const double hh = 0.5 * h;
+#if BHRT_FOLD_SIXTH
+    const double h6 = h * (1.0 / 6.0);
+#endif
     rhs<SPIN0, FAR, HUGE>(y, k, sc, far_ok, n, tr, true);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
@@ -336,7 +415,15 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
     }
     rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
-    for (int i = 0; i < 6; i++) y[i] += div6(h * (acc[i] + k[i]));
+    for (int i = 0; i < 6; i++) {
+#if BHRT_FOLD_SIXTH
+        // h * (...) / 6 as (h * RN(1/6)) * (...): the increment differs by <= 1 ulp of itself,
+        // which is ~h*|k| / |y| ulp of the state (A/B variant "nosixth" keeps the division)
+        y[i] = __builtin_fma(h6, acc[i] + k[i], y[i]);
+#else
+        y[i] += div6(h * (acc[i] + k[i]));
+#endif
+    }
 }
 
 // rkf45_integrate (math_util.c:212-457), n = 6. Returns true on accept (y <- y5).
@@ -420,12 +507,9 @@ __device__ __forceinline__ void sph2cart_t(double r, double st, double ct, doubl
 __device__ __forceinline__ void trig_advance(double a, double x, double& s, double& c,
                                              Counters* hc) {
     double s1, c1;
-    if (sincos_shift(a, s, c, x, s1, c1)) {
-        s = s1;
-        c = c1;
-    } else {
-        bhrt_sincos(x, &s, &c, hc);
-    }
+    shift_or_eval(a, s, c, x, s1, c1, hc);
+    s = s1;
+    c = c1;
 }
 
 __device__ __forceinline__ double len3(double x, double y, double z) {
@@ -629,6 +713,11 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     double x, y, z;
 #if BHRT_TRIG_CHAIN
     if (moved) {
+#if BHRT_STATS
+        dstat(n, 3, R.y[1] - tr.a);
+        dstat(n, 4, R.y[2] - a2);
+        dstat(n, 5, R.y[3] - a3);
+#endif
         trig_advance(tr.a, R.y[1], R.s1, R.c1, hc);
         trig_advance(a2, R.y[2], R.s2, R.c2, hc);
         trig_advance(a3, R.y[3], R.s3, R.c3, hc);
@@ -827,6 +916,12 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             if (exhausted) break;
             continue;
         }
+#if BHRT_STATS
+        if (lane == 0) {
+            n.ds[60]++;
+            n.ds[61] += n_live;
+        }
+#endif
         if (live) {
             const int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n);
             if (!HUGE && n.huge) {  // hand the ray to the HUGE instantiation
@@ -850,6 +945,12 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         if (s3) atomicAdd(kp.ctl + 4, s3);
         if (s4) atomicAdd(kp.ctl + 5, s4);
     }
+#if BHRT_STATS
+    for (int j = 0; j < BHRT_STATS_N; j++) {
+        const unsigned long long v = wave_sum(n.ds[j]);
+        if (lane == 0 && v) atomicAdd(&g_dstats[j], v);
+    }
+#endif
 }
 
 __device__ __forceinline__ double clampd(double v, double lo, double hi) {
@@ -1069,6 +1170,19 @@ extern "C" int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0
     default: return dispatch_disk<INTEGRATOR_LEAPFROG>(*kp, st, e0, e1);  // no-op integrators
     }
 }
+
+#if BHRT_STATS
+extern "C" __attribute__((visibility("default"))) int bhrt_debug_stats(unsigned long long* out,
+                                                                      int reset) {
+    int rc = (int)hipDeviceSynchronize();
+    if (!rc) rc = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dstats), sizeof(g_dstats));
+    if (!rc && reset) {
+        static const unsigned long long zero[BHRT_STATS_N] = {};
+        rc = (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dstats), zero, sizeof(zero));
+    }
+    return rc;
+}
+#endif
 
 extern "C" int bhrt_launch_path(const bhrt_kparams* kp, const double* o4, const double* d3,
                                 Vector3D* d_path, int max_positions, int* d_num, int num_in,

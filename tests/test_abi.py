@@ -185,10 +185,10 @@ def build_c_demo(tmp_path):
     names (include/blackhole_api.h etc. forward to bhrt_api.h), and link it to libbhrt.so."""
     import subprocess
     exe = str(tmp_path / "trace_demo")
-    libdir = os.path.dirname(lib.LIB_PATH)
+    path = os.path.abspath(lib.LIB_PATH)  # BHRT_LIB may name an A/B build (ab/libbhrt_*.so)
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "examples", "trace_demo.c"), "-L", libdir, "-lbhrt",
-                    f"-Wl,-rpath,{libdir}", "-lm", "-o", exe], check=True)
+                    os.path.join(ROOT, "examples", "trace_demo.c"), path,
+                    f"-Wl,-rpath,{os.path.dirname(path)}", "-lm", "-o", exe], check=True)
     return exe
 
 
