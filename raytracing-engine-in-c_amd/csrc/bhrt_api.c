@@ -314,10 +314,11 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
     s->rs_x5 = rs * 5.0;
     s->rs_x15 = rs * 15.0;
     s->rs_eps = rs + BH_EPSILON;
-    s->h_2_5 = dt * 0.001;
-    s->h_5 = dt * 0.01;
-    s->h_15 = dt * 0.1;
-    s->h_far = dt;
+    /* the schedule's candidates with fmin(h, 0.1) applied (raytracer.c:556-571) */
+    s->h_2_5 = fmin(dt * 0.001, 0.1);
+    s->h_5 = fmin(dt * 0.01, 0.1);
+    s->h_15 = fmin(dt * 0.1, 0.1);
+    s->h_far = fmin(dt, 0.1);
     s->max_dist = cfg->max_ray_distance;
     s->tol = cfg->tolerance;
     s->max_steps = cfg->max_integration_steps;

@@ -280,6 +280,9 @@ struct Trig1 {
 #ifndef BHRT_LAZY_CLAMP
 #define BHRT_LAZY_CLAMP 1
 #endif
+#ifndef BHRT_REASSOC
+#define BHRT_REASSOC 1
+#endif
 #ifndef BHRT_FOLD_SIXTH
 #define BHRT_FOLD_SIXTH 1
 #endif
@@ -289,6 +292,62 @@ struct Trig1 {
 #ifndef BHRT_TEST_D012
 #define BHRT_TEST_D012 0
 #endif
+// ray_derivatives' a = 0 accelerations in the literal form (:92-130, evaluation order as
+// written, divisions as div_nr / IEEE), from sin, cos of the unclamped theta.
+template <bool UNUSED = false>
+__device__ __forceinline__ void accel_literal(const double (&y)[6], double (&d)[6], const Scene& sc,
+                                              double st, double ct) {
+    double r = y[0];
+    double rsq = r * r;
+    double st2 = st * st;
+    if (r <= sc.rs_x1_5) {
+        r = sc.rs_x1_5;
+        rsq = r * r;
+    }
+    if (fabs(st) < 0.01) {
+        st = (st >= 0.0) ? 0.01 : -0.01;
+        st2 = st * st;
+    }
+    const double term2 = r * y[4] * y[4];
+    const double term3 = r * st2 * y[5] * y[5];
+    const double n4 = -2.0 * y[3] * y[4];
+    const double n5a = -2.0 * y[3] * y[5];
+    const double n5b = 2.0 * y[4] * y[5] * ct;
+    const double sc4 = st * ct * y[5] * y[5];
+    if (r < 1.0e150) {  // r >= 1.5 rs here: every divisor is in the normal range
+        const double yr = rcp_nr(r);
+#if BHRT_FOLD_TERM1
+        // -M / (r^2 f) * f == -M / r^2 in exact arithmetic (A/B variant "nofold" keeps it)
+        const double term1 = -(sc.M * yr) * yr;
+#else
+        const double f = 1.0 - div_nr(sc.rs, r, yr);
+        const double den = rsq * f;
+        const double term1 = -div_nr(sc.M, den, rcp_nr(den)) * f;
+#endif
+        d[3] = term1 + term2 + term3;
+        d[4] = div_nr(n4, r, yr) + sc4;
+        d[5] = div_nr(n5a, r, yr) - div_nr(n5b, st, rcp_nr(st));
+    } else {
+        const double f = 1.0 - sc.rs / r;
+        const double term1 = -sc.M / (rsq * f) * f;
+        d[3] = term1 + term2 + term3;
+        d[4] = n4 / r + sc4;
+        d[5] = n5a / r - n5b / st;
+    }
+}
+
+// :141-153 -- non-finite -> 0 for all six, then |d[3..5]| <= 10.
+__device__ __forceinline__ void repair_clamp(double (&d)[6]) {
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+        if (!isfinite(d[i])) d[i] = 0.0;
+#pragma unroll
+    for (int i = 3; i < 6; i++) d[i] = fmin(fmax(d[i], -10.0), 10.0);
+}
+
+// ray_derivatives (raytracer.c:44-154) for one RK stage; see the block comment above Trig1.
+// Stage counters: only FAR instantiations count per stage (a lane's branch varies); otherwise
+// every stage takes the one branch of the instantiation and k_trace derives the count.
 template <bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const Scene& sc,
                                     bool far_ok, Counters& n, Trig1& tr, bool first) {
@@ -303,8 +362,6 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         return;
     }
     if (SPIN0) {  // :92-130
-        double r = y[0];
-        double rsq = r * r;
         double st, ct;
         if (first) {
 #if BHRT_TRIG_CHAIN
@@ -322,49 +379,41 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
 #endif
             shift_or_eval(tr.a, tr.s, tr.c, y[1], st, ct, HUGE ? nullptr : &n);
         }
-        double st2 = st * st;
-        if (r <= sc.rs_x1_5) {
-            r = sc.rs_x1_5;
-            rsq = r * r;
-        }
-        if (fabs(st) < 0.01) {
-            st = (st >= 0.0) ? 0.01 : -0.01;
-            st2 = st * st;
-        }
-        const double term2 = r * y[4] * y[4];
-        const double term3 = r * st2 * y[5] * y[5];
-        const double n4 = -2.0 * y[3] * y[4];
-        const double n5a = -2.0 * y[3] * y[5];
-        const double n5b = 2.0 * y[4] * y[5] * ct;
-        const double sc4 = st * ct * y[5] * y[5];
-        if (r < 1.0e150) {  // r >= 1.5 rs here: every divisor is in the normal range
-            const double yr = rcp_nr(r);
-#if BHRT_FOLD_TERM1
-            // -M / (r^2 f) * f == -M / r^2 in exact arithmetic (A/B variant "fold")
-            const double term1 = -(sc.M * yr) * yr;
+        if (FAR) n.full++;
+#if BHRT_REASSOC
+        // Fast form, straight-line: the same three accelerations with the divisions as two
+        // reciprocals and the products regrouped -- d3 = -M/r^2 + r (v_th^2 + (sin th v_ph)^2),
+        // d4 = -2 v_r v_th / r + (sin th v_ph)(cos th v_ph),
+        // d5 = -2 v_ph (v_r / r + v_th cos th / sin th) -- a few ulp from the literal
+        // expressions. y[0] is finite (the state is repaired at the top
+        // of every iteration and a stage adds a bounded increment), so fmax is the reference's
+        // clamp. A lane whose result is not a plain |d| <= 10 value (never on a C2 frame)
+        // recomputes it in the literal form before the repair and clamps.
+        const double rc = fmax(y[0], sc.rs_x1_5);
+        double sc_ = st;
+        if (fabs(st) < 0.01) sc_ = (st >= 0.0) ? 0.01 : -0.01;
+        const double yr = rcp_nr(rc), ys = rcp_nr(sc_);
+        const double u = sc_ * y[5];
+        const double f3 = rc * __builtin_fma(u, u, y[4] * y[4]);
+        d[3] = __builtin_fma(-(sc.M * yr), yr, f3);
+        const double p = y[3] * yr;
+        d[4] = __builtin_fma(p * -2.0, y[4], u * (ct * y[5]));
+        d[5] = (y[5] * -2.0) * __builtin_fma(y[4], ct * ys, p);
+        const int plain = (int)(rc < 1.0e150) & (int)(fabs(d[3]) <= 10.0) &
+                          (int)(fabs(d[4]) <= 10.0) & (int)(fabs(d[5]) <= 10.0);
+        if (__builtin_expect(plain, 1)) return;
+        accel_literal(y, d, sc, st, ct);
+        repair_clamp(d);
+        return;
 #else
-            const double f = 1.0 - div_nr(sc.rs, r, yr);
-            const double den = rsq * f;
-            const double term1 = -div_nr(sc.M, den, rcp_nr(den)) * f;
+        accel_literal(y, d, sc, st, ct);
 #endif
-            d[3] = term1 + term2 + term3;
-            d[4] = div_nr(n4, r, yr) + sc4;
-            d[5] = div_nr(n5a, r, yr) - div_nr(n5b, st, rcp_nr(st));
-        } else {
-            const double f = 1.0 - sc.rs / r;
-            const double term1 = -sc.M / (rsq * f) * f;
-            d[3] = term1 + term2 + term3;
-            d[4] = n4 / r + sc4;
-            d[5] = n5a / r - n5b / st;
-        }
-        n.full++;
     } else {  // :131-138
         d[3] = 0.0;
         d[4] = 0.0;
         d[5] = 0.0;
-        n.kerr++;
+        if (FAR) n.kerr++;
     }
-    // :141-153 -- non-finite -> 0 for all six, then |d[3..5]| <= 10.
 #if BHRT_LAZY_CLAMP
     // Neither ever applies on a C2 frame (none of 8.3e7 evaluations): one test
     // per component (NaN and Inf fail |d| <= 10) sends the rare lane through the literal repair.
@@ -378,11 +427,7 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
 #endif
     if (plain) return;
 #endif
-#pragma unroll
-    for (int i = 0; i < 6; i++)
-        if (!isfinite(d[i])) d[i] = 0.0;
-#pragma unroll
-    for (int i = 3; i < 6; i++) d[i] = fmin(fmax(d[i], -10.0), 10.0);
+    repair_clamp(d);
 }
 
 // rk4_integrate (math_util.c:162-207) on the six live components; the running sum
@@ -512,8 +557,28 @@ __device__ __forceinline__ void trig_advance(double a, double x, double& s, doub
     c = c1;
 }
 
+// sqrt as the compiler's f64 expansion computes it (v_rsq_f64, Goldschmidt refinement, two
+// residual corrections) without its denormal scaling and Inf/0 class fix-up, which only
+// x < 2^-767 needs -- those lanes take the library sqrt.
+__device__ __forceinline__ double sqrt_nr(double x) {
+    if (__builtin_expect(!(x >= 0x1p-767), 0)) return sqrt(x);
+    const double y = __builtin_amdgcn_rsq(x);
+    double s = x * y, hy = y * 0.5;
+    const double r = __builtin_fma(-hy, s, 0.5);
+    s = __builtin_fma(s, r, s);
+    hy = __builtin_fma(hy, r, hy);
+    double e = __builtin_fma(-s, s, x);
+    s = __builtin_fma(e, hy, s);
+    e = __builtin_fma(-s, s, x);
+    return __builtin_fma(e, hy, s);
+}
+
 __device__ __forceinline__ double len3(double x, double y, double z) {
     return sqrt((x * x + y * y) + z * z);  // vector3D_length (math_util.c:85-113)
+}
+// the per-iteration path length |p - p_prev| of the hot loop
+__device__ __forceinline__ double seg_len(double x, double y, double z) {
+    return sqrt_nr((x * x + y * y) + z * z);
 }
 
 struct Ray_ {
@@ -692,10 +757,9 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     double h = sc.h_far;
     h = (r < sc.rs_x15) ? sc.h_15 : h;
     h = (r < sc.rs_x5) ? sc.h_5 : h;
-    h = (r < sc.rs_x2_5) ? sc.h_2_5 : h;
-    h = fmin(h, 0.1);
+    h = (r < sc.rs_x2_5) ? sc.h_2_5 : h;  // fmin(h, 0.1) is folded into the four values (host)
     bool moved = true;
-    n.iters++;
+    if (METHOD != INTEGRATOR_RK4) n.iters++;  // RK4: counted at termination (k_trace)
     Trig1 tr;
 #if BHRT_TRIG_CHAIN
     tr.a = R.y[1];
@@ -727,7 +791,7 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     sph2cart(R.y[1], R.y[2], R.y[3], x, y, z, hc);
 #endif
     const double ox = R.px, oy = R.py, oz = R.pz;
-    R.dist += len3(x - ox, y - oy, z - oz);
+    R.dist += seg_len(x - ox, y - oy, z - oz);
     R.px = x;
     R.py = y;
     R.pz = z;
@@ -924,6 +988,8 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
 #endif
         if (live) {
             const int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n);
+            if (METHOD == INTEGRATOR_RK4 && (term != T_NONE || (!HUGE && n.huge)))
+                n.iters += R.k;  // every RK4 iteration moves, so R.k = iterations executed
             if (!HUGE && n.huge) {  // hand the ray to the HUGE instantiation
                 n.huge = false;
                 n.rays--;
@@ -936,8 +1002,17 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         }
     }
     const unsigned long long s0 = wave_sum(n.rays), s1 = wave_sum(n.iters),
-                             s2 = wave_sum(n.full), s3 = wave_sum(n.far_),
-                             s4 = wave_sum(n.kerr);
+                             s3 = wave_sum(n.far_);
+    unsigned long long s2, s4;
+    if (FAR) {  // stages counted one by one
+        s2 = wave_sum(n.full);
+        s4 = wave_sum(n.kerr);
+    } else {    // every stage took the instantiation's branch
+        const unsigned long long st =
+            s1 * (METHOD == INTEGRATOR_RK4 ? 4ull : (METHOD == INTEGRATOR_RKF45 ? 6ull : 0ull));
+        s2 = SPIN0 ? st : 0ull;
+        s4 = SPIN0 ? 0ull : st;
+    }
     if (lane == 0) {
         if (s0) atomicAdd(kp.ctl + 1, s0);
         if (s1) atomicAdd(kp.ctl + 2, s1);
