@@ -133,6 +133,14 @@ __device__ __forceinline__ double fmac_k(double a, double b, double c) {
 #endif
 }
 
+// max(a, b) as ONE v_max_f64 (b in SGPRs): fmax would first canonicalize both operands
+// (v_max_f64 x, x, x) for its NaN rule; callers pass non-NaN a.
+__device__ __forceinline__ double max_raw(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "s"(b));
+    return r;
+}
+
 // sin and cos of one argument, for the trace loop. OCML's sincos
 // spends ~78 VALU per call on a range reduction valid to 2^30+; every argument here (the
 // radius read as an angle by ray_derivatives, theta, phi) stays far below 2^20, where a
@@ -254,7 +262,9 @@ __device__ __forceinline__ void shift_or_eval(double a, double s0, double c0, do
     const double cm1 = z * __builtin_fma(z, fmac_k(z, fmac_k(z, C3, C2), C1), -0.5);
     s = s0 + (s0 * cm1 + c0 * sd);
     c = c0 + (c0 * cm1 - s0 * sd);
-    if (__builtin_expect(!(fabs(delta) <= 0.0625 && fabs(delta) <= 0.5 * fabs(a)), 0)) {
+    // (delta = x - a is exact for |x - a| <= |a| / 2 (Sterbenz); otherwise -- a near 0 -- it is
+    // off by <= ulp(delta) / 2 <= 3.5e-18, well below the polynomials' rounding)
+    if (__builtin_expect(!(fabs(delta) <= 0.0625), 0)) {
         if (!sincos_shift_wide(a, s0, c0, x, s, c)) bhrt_sincos(x, &s, &c, hc);
     }
 #else
@@ -279,6 +289,9 @@ struct Trig1 {
 // HUGE: keep the large-argument sincos path (else flag it, see bhrt_sincos)
 #ifndef BHRT_LAZY_CLAMP
 #define BHRT_LAZY_CLAMP 1
+#endif
+#ifndef BHRT_ONE_RCP
+#define BHRT_ONE_RCP 0
 #endif
 #ifndef BHRT_REASSOC
 #define BHRT_REASSOC 1
@@ -389,10 +402,16 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         // of every iteration and a stage adds a bounded increment), so fmax is the reference's
         // clamp. A lane whose result is not a plain |d| <= 10 value (never on a C2 frame)
         // recomputes it in the literal form before the repair and clamps.
-        const double rc = fmax(y[0], sc.rs_x1_5);
+        const double rc = max_raw(y[0], sc.rs_x1_5);
         double sc_ = st;
         if (fabs(st) < 0.01) sc_ = (st >= 0.0) ? 0.01 : -0.01;
+#if BHRT_ONE_RCP
+        // 1/r and 1/sin theta from one reciprocal of the product (r sin theta in [0.03, 1e150])
+        const double w = rcp_nr(rc * sc_);
+        const double yr = sc_ * w, ys = rc * w;
+#else
         const double yr = rcp_nr(rc), ys = rcp_nr(sc_);
+#endif
         const double u = sc_ * y[5];
         const double f3 = rc * __builtin_fma(u, u, y[4] * y[4]);
         d[3] = __builtin_fma(-(sc.M * yr), yr, f3);
