@@ -91,12 +91,22 @@ __device__ __forceinline__ void dstat(Counters& n, int site, double delta) {
 // and the hit points as close (profiles/r01_bench_all_configs_v6.jsonl), for 7% of C2.
 // BHRT_EXACT_DIV=1 adds the quotient's residual correction, which makes it bit-identical
 // to a / b (the A/B build "exdiv"). Callers keep the IEEE a / b for out-of-range operands.
+// BHRT_RCP3 (default): one cubically convergent step y0 (1 + e + e^2) instead of two Newton
+// steps -- v_rcp_f64 is good to ~2^-24 (tools/probe/trans_probe.hip), so e^3 ~ 2^-72 is far below
+// the final rounding: the same <= 1 ulp quotient for three FMAs instead of four.
+#ifndef BHRT_RCP3
+#define BHRT_RCP3 1
+#endif
 __device__ __forceinline__ double rcp_nr(double b) {
     double y = __builtin_amdgcn_rcp(b);
     double e = __builtin_fma(-b, y, 1.0);
+#if BHRT_RCP3
+    return __builtin_fma(y, __builtin_fma(e, e, e), y);
+#else
     y = __builtin_fma(y, e, y);
     e = __builtin_fma(-b, y, 1.0);
     return __builtin_fma(y, e, y);
+#endif
 }
 #ifndef BHRT_EXACT_DIV
 #define BHRT_EXACT_DIV 0
@@ -249,6 +259,9 @@ __device__ __forceinline__ bool sincos_shift_wide(double a, double s0, double c0
 #ifndef BHRT_SHORT_SHIFT
 #define BHRT_SHORT_SHIFT 1
 #endif
+#ifndef BHRT_SHIFT_FMA2
+#define BHRT_SHIFT_FMA2 1
+#endif
 __device__ __forceinline__ void shift_or_eval(double a, double s0, double c0, double x, double& s,
                                               double& c, Counters* hc) {
 #if BHRT_SHORT_SHIFT
@@ -260,8 +273,14 @@ __device__ __forceinline__ void shift_or_eval(double a, double s0, double c0, do
     const double z = delta * delta;
     const double sd = delta + (z * delta) * fmac_k(z, fmac_k(z, S3, S2), S1);  // sin(delta)
     const double cm1 = z * __builtin_fma(z, fmac_k(z, fmac_k(z, C3, C2), C1), -0.5);
+#if BHRT_SHIFT_FMA2
+    // s0 (1 + cm1) + c0 sd as two FMAs (<= 1 ulp instead of ~0.5)
+    s = __builtin_fma(c0, sd, __builtin_fma(s0, cm1, s0));
+    c = __builtin_fma(-s0, sd, __builtin_fma(c0, cm1, c0));
+#else
     s = s0 + (s0 * cm1 + c0 * sd);
     c = c0 + (c0 * cm1 - s0 * sd);
+#endif
     // (delta = x - a is exact for |x - a| <= |a| / 2 (Sterbenz); otherwise -- a near 0 -- it is
     // off by <= ulp(delta) / 2 <= 3.5e-18, well below the polynomials' rounding)
     if (__builtin_expect(!(fabs(delta) <= 0.0625), 0)) {
