@@ -1,9 +1,9 @@
 """Benchmark of the geodesic ray-tracing hot path (BASELINE.json metric) on MI355X.
 
 One "step" = one camera frame of the workload traced by libbhrt.so with every input already
-on the device: the frame kernel launch, plus (N > 1) the single RCCL gather of all ranks'
-buffers to rank 0 and its assembly there (bhrt/dist_frame.py FramePipeline; the gather of
-frame i overlaps the rendering of frame i+1, and the timed region ends after the last one).
+on the device: the frame kernel launch, plus (N > 1) the frame's single RCCL collective and
+its assembly on rank 0 (bhrt/dist_frame.py FramePipeline; the collective of frame i overlaps
+the rendering of frame i+1, and the timed region ends after the last one).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--camera B]
 
@@ -11,7 +11,8 @@ N > 1 is launched by torch.distributed.run, one process per GPU.
   * Weak scaling (C1, C2, C3, C5): every GPU traces the whole configuration frame (1920 x 1080
     for C2) at its own sub-pixel offset -- rank 0 the pixel centres, rank k the reference's
     Halton sample k (trace_pixel's jitter) -- so N GPUs supersample the frame with N samples
-    per pixel and every GPU does exactly one frame's work; rank 0 averages the colour.
+    per pixel and every GPU does exactly one frame's work; one RCCL reduce sums the colour
+    planes on rank 0, which divides by N (trace_pixel's sample average, raytracer.c:1096-1164).
     (A taller image 1080*N rows high is NOT used: with the fixed vertical FOV its horizontal
     FOV shrinks with N and the per-ray work collapses -- 400 -> 1.6 iterations/ray at N=8.)
   * Strong scaling (C4): one 3840 x 2160 image split into cyclic 8-row blocks (block b ->
@@ -172,8 +173,9 @@ def main():
                              "gather to rank 0 per frame (overlapped with the next frame)")
                             if strong else
                             (f"dp{world}: one sub-pixel sample plane of the frame per GPU "
-                             f"({world} samples/pixel), one RCCL gather to rank 0 per frame "
-                             "(overlapped with the next frame)")),
+                             f"({world} samples/pixel), one RCCL reduce of the colour planes "
+                             "to rank 0 per frame (the sample average, overlapped with the "
+                             "next frame)")),
         },
         "rk4_steps_per_s": round(iterations_all * (1.0 / elapsed), 1),
         "per_gpu_mrays_s": round(mrays / world, 3),

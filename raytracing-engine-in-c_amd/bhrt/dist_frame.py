@@ -9,11 +9,14 @@ gloo in the CPU tests). Two ways of splitting the work (FramePipeline.mode):
     permutes the gathered shards back to image order on the device.
   * "samples" (weak scaling): every rank traces the whole frame at its own sub-pixel offset
     (sample_offset: rank 0 the pixel centre, rank k the reference's Halton point k), i.e.
-    the frame is supersampled across GPUs with the per-GPU work of one frame; rank 0 keeps
-    the per-sample planes and averages their colour.
+    the frame is supersampled across GPUs with the per-GPU work of one frame -- trace_pixel's
+    supersampling (raytracer.c:1096-1164) with one sample per GPU. Its exchange is the
+    sample average of the colour: ONE reduce (sum) of the three colour planes to rank 0
+    (24 B per ray instead of the 96 B of a full gather), which divides by the sample count.
+    Every rank's per-ray SoA (hit classes, points, distances) stays resident on its own GPU.
 
-The gather of frame i runs (on the collective's own stream) while frame i+1 renders; a
-buffer is reused only after the gather that read it has completed (double buffering).
+The collective of frame i runs (on the collective's own stream) while frame i+1 renders; a
+buffer is reused only after the collective that read it has completed (double buffering).
 """
 import numpy as np
 import torch
@@ -22,6 +25,7 @@ import torch.distributed as dist
 from . import abi
 
 INT_FIELDS = ("result", "steps")
+RGB_FIELDS = ("rgb_r", "rgb_g", "rgb_b")
 
 
 def shard_row_count(H, row_block, shard, world):
@@ -113,8 +117,9 @@ class FramePipeline:
     Per frame: fb = next_buffer(); render into fb; submit(). finish() completes the gathers
     still in flight and returns rank 0's newest assembled frame (None elsewhere):
       shards:  {field: [H, W]}
-      samples: {field: [world, H, W]} plus, for world > 1, "rgb_mean" [3, H, W] when rgb
-               was rendered (one plane is its own mean).
+      samples: world > 1 with rgb rendered: {field: [1, H, W]} of rank 0's own sample plane
+               plus "rgb_mean" [3, H, W], the colour averaged over all planes (reduce);
+               without rgb: {field: [world, H, W]}, every plane gathered; world 1: the plane.
     """
 
     def __init__(self, n, device, world, rank, mode, H, W, row_block=8,
@@ -123,8 +128,13 @@ class FramePipeline:
         self.world, self.rank, self.mode = world, rank, mode
         self.H, self.W, self.row_block = H, W, row_block
         self.bufs = [FrameBuffer(n, device, fields) for _ in range(2)]
+        self.reduce = (mode == "samples" and world > 1 and
+                       all(c in fields for c in RGB_FIELDS))
+        if self.reduce:  # per slot: the colour planes summed over ranks (in place on rank 0)
+            self.colour = [torch.empty(3, n, dtype=torch.float64, device=device)
+                           for _ in range(2)]
         self.gathered = ([[torch.empty_like(b.buf) for _ in range(world)] for b in self.bufs]
-                         if (world > 1 and rank == 0) else None)
+                         if (world > 1 and rank == 0 and not self.reduce) else None)
         self.works = [None, None]
         self.frames = 0
         self.last = None
@@ -136,7 +146,12 @@ class FramePipeline:
 
     def submit(self):
         slot = self.frames % 2
-        if self.world > 1:
+        if self.reduce:
+            fb, col = self.bufs[slot], self.colour[slot]
+            for i, c in enumerate(RGB_FIELDS):
+                col[i].copy_(fb.views[c])
+            self.works[slot] = dist.reduce(col, dst=0, op=dist.ReduceOp.SUM, async_op=True)
+        elif self.world > 1:
             self.works[slot] = dist.gather(
                 self.bufs[slot].buf, self.gathered[slot] if self.rank == 0 else None, dst=0,
                 async_op=True)
@@ -161,7 +176,7 @@ class FramePipeline:
 
     def _assemble(self, slot):
         fb, H, W, world = self.bufs[slot], self.H, self.W, self.world
-        parts = self.gathered[slot] if world > 1 else [fb.buf]
+        parts = self.gathered[slot] if (world > 1 and not self.reduce) else [fb.buf]
         img = {}
         if self.mode == "shards":
             if world == 1:
@@ -172,10 +187,13 @@ class FramePipeline:
                 img[f] = (p.view(world, n_rows // B, B, W).permute(1, 0, 2, 3)
                           .reshape(world * n_rows, W)[:H])
             return img
+        if self.reduce:  # rank 0's own plane (sample 0) and the mean colour of all samples
+            img = {f: fb.views[f].view(1, H, W) for f in fb.fields}
+            img["rgb_mean"] = (self.colour[slot] / world).view(3, H, W)
+            return img
         for f in fb.fields:
             img[f] = (fb.views[f].view(1, H, W) if world == 1 else
                       torch.stack([fb.view(g, f) for g in parts]).view(world, H, W))
-        if world > 1 and all(c in img for c in ("rgb_r", "rgb_g", "rgb_b")):
-            img["rgb_mean"] = torch.stack([img[c].mean(dim=0)
-                                           for c in ("rgb_r", "rgb_g", "rgb_b")])
+        if world > 1 and all(c in img for c in RGB_FIELDS):
+            img["rgb_mean"] = torch.stack([img[c].mean(dim=0) for c in RGB_FIELDS])
         return img

@@ -139,7 +139,8 @@ def _pipeline_worker(rank, world, port, mode, W, H, frames, out_path):
 
 @pytest.mark.parametrize("world,mode,frames,H", [(2, "shards", 3, 24), (3, "shards", 4, 24),
                                                  (2, "shards", 2, 20), (3, "shards", 3, 26),
-                                                 (2, "samples", 3, 24), (3, "samples", 1, 24)])
+                                                 (2, "samples", 3, 24), (3, "samples", 1, 24),
+                                                 (4, "samples", 3, 16)])
 def test_pipelined_gather(tmp_path, oracle, world, mode, frames, H):
     W = 16
     out = str(tmp_path / "frame.npz")
@@ -161,10 +162,11 @@ def test_pipelined_gather(tmp_path, oracle, world, mode, frames, H):
             if off is not None:
                 cam_k.use_offset, cam_k.offset_x, cam_k.offset_y = 1, off[0], off[1]
             planes.append(oracle.render_frame(bh, dk, cfg, cam_k, W, H, c.method, c.flags))
-        for k, p in enumerate(planes):
-            for f in abi.SOA_FIELDS:
-                w = p[f] + (frames - 1) if f == "steps" else p[f]
-                assert np.array_equal(got[f][k].reshape(-1), w, equal_nan=True), (k, f)
+        for f in abi.SOA_FIELDS:  # rank 0 keeps its own plane (sample 0) ...
+            w = planes[0][f] + (frames - 1) if f == "steps" else planes[0][f]
+            assert got[f].shape[0] == 1
+            assert np.array_equal(got[f][0].reshape(-1), w, equal_nan=True), f
+        # ... and receives the colour averaged over every rank's plane (one reduce)
         mean = np.stack([np.mean([p[ch] for p in planes], axis=0)
                          for ch in ("rgb_r", "rgb_g", "rgb_b")])
         np.testing.assert_allclose(got["rgb_mean"].reshape(3, -1), mean, rtol=1e-12)
