@@ -3,7 +3,10 @@
 One "step" = one camera frame of the workload traced by libbhrt.so with every input already
 on the device: the frame kernel launch, plus (N > 1) the frame's single RCCL collective and
 its assembly on rank 0 (bhrt/dist_frame.py FramePipeline; the collective of frame i overlaps
-the rendering of frame i+1, and the timed region ends after the last one).
+the rendering of frame i+1, and the timed region ends after the last one). Consecutive frames
+alternate between two HIP streams (--streams 2, the default), so the workgroups of frame i+1
+take the CUs that frame i's tail -- its last, longest rays draining -- leaves idle
+(tools/wave_tail.py: ~9% of a lone C2 launch); --streams 1 runs the frames back to back.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--camera B]
 
@@ -21,7 +24,9 @@ N > 1 is launched by torch.distributed.run, one process per GPU.
 The JSON line also carries:
   roofline      FP64 VALU roofline of the trace kernel: algorithmic FLOPs (SURVEY.md 8(a):
                 117 per RK4 iteration + 35 per a=0 derivative stage + 4 per far-field stage;
-                368 per RKF45 attempt + the same stage costs) / the kernel's HIP-event time.
+                368 per RKF45 attempt + the same stage costs) / the kernel's GPU time per
+                launch: with overlapping frames the HIP-event busy span of the timed launches
+                (first start to last end) / launches, else the per-launch HIP-event average.
   cpu_baseline  the compiled reference (oracle/_ref/libref.so, unmodified trace_ray under an
                 OpenMP loop) on a row sample of the same frame, rank 0 at N = 1 only; its
                 sampled rows double as the parity check "max |dhit|".
@@ -62,6 +67,9 @@ def parse():
     p.add_argument("--no-host-path", action="store_true",
                    help="skip the host-buffer leg (its chunked launches would mix into a "
                         "profiler's per-launch kernel averages)")
+    p.add_argument("--streams", type=int, default=2,
+                   help="consecutive frames alternate between this many HIP streams, so the "
+                        "next frame's rays fill the CUs the tail of the current frame frees")
     p.add_argument("--sample", type=int, default=None,
                    help="weak scaling: trace sample plane K instead of this rank's (to time "
                         "each plane of an N-GPU run on one GPU)")
@@ -78,6 +86,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.streams not in (1, 2):  # FramePipeline has two buffer slots, one per stream
+        raise SystemExit("--streams must be 1 or 2")
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
@@ -104,13 +114,22 @@ def main():
             cam.use_offset, cam.offset_x, cam.offset_y = 1, off[0], off[1]
     pipe = FramePipeline(n, device, world, rank, "shards" if strong else "samples", H, W,
                          ROW_BLOCK, FIELDS)
-    stream = torch.cuda.current_stream()
+    streams = ([torch.cuda.current_stream()] if args.streams <= 1 else
+               [torch.cuda.Stream(device) for _ in range(args.streams)])
+    frame_no = [0]
 
     def step():
-        fb = pipe.next_buffer()
-        lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags, fb.soa(),
-                                stream.cuda_stream)
-        pipe.submit()
+        # Frame k renders on streams[k % S]. A persistent k_trace launch ends with a tail in
+        # which its last (up to max_steps-iteration) rays drain and CUs fall idle; with S > 1
+        # the next frame's workgroups take those CUs (tools/wave_tail.py measures the tail).
+        # A frame buffer slot is reused two frames later, on the same stream when S = 2.
+        s = streams[frame_no[0] % len(streams)]
+        frame_no[0] += 1
+        with torch.cuda.stream(s):
+            fb = pipe.next_buffer()
+            lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags, fb.soa(),
+                                    s.cuda_stream)
+            pipe.submit()
 
     for _ in range(args.warmup):
         step()
@@ -145,9 +164,16 @@ def main():
 
     rays_all = float(W * H) * args.steps * (1 if strong else world)
     mrays = rays_all / elapsed / 1e6
-    kern_ms = st["kernel_ms"] / max(st["launches"], 1)
-    f_launch = flops(st, c.method) / max(st["launches"], 1)
-    achieved = f_launch / (kern_ms * 1e-3) / 1e12
+    launches = max(st["launches"], 1)
+    kern_ms = st["kernel_ms"] / launches
+    # GPU time per trace launch: the per-launch HIP-event duration when frames run one after
+    # another; with frames alternating between two streams consecutive launches overlap (the
+    # next frame fills the CUs the current one's tail frees) and each launch's own start..end
+    # interval double-counts the overlap, so the busy span of all timed launches / launches
+    span_ms = st["span_ms"] / launches
+    dur_ms = span_ms if len(streams) > 1 else kern_ms
+    f_launch = flops(st, c.method) / launches
+    achieved = f_launch / (dur_ms * 1e-3) / 1e12
     out = {
         "metric": METRIC,
         "value": round(mrays, 3),
@@ -181,7 +207,12 @@ def main():
         "per_gpu_mrays_s": round(mrays / world, 3),
         "kernel": {
             "name": "k_trace (persistent, wave refill)",
-            "avg_ms": round(kern_ms, 4),
+            "avg_ms": round(dur_ms, 4),
+            "duration": ("busy span of the timed launches (HIP events, first start to last "
+                         "end) / launches: frames alternate between 2 streams and overlap"
+                         if len(streams) > 1 else "per-launch HIP-event duration, averaged"),
+            "event_avg_ms": round(kern_ms, 4),
+            "streams": len(streams),
             "iterations_per_launch": st["iterations"] / max(st["launches"], 1),
             "mean_iterations_per_ray": st["iterations"] / max(st["rays"], 1),
         },

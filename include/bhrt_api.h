@@ -264,6 +264,9 @@ typedef struct {
     uint64_t launches;      /* trace-kernel launches timed                               */
     double   kernel_ms;     /* sum of HIP-event durations of those launches              */
     uint64_t rays_redone;   /* rays re-traced on the large-argument sincos path          */
+    double   span_ms;       /* per GPU: first trace-kernel start to last trace-kernel end
+                               since the reset (summed over GPUs); launches overlapping on
+                               several streams make this, not kernel_ms, the GPU time     */
 } bhrt_stats;
 
 /* Number of rows of an image of `height` rows owned by shard rows->shard. */

@@ -125,6 +125,13 @@ typedef struct {
      * copy stream, and per chunk: trace finished / its D2H landed */
     hipStream_t stream2, copy;
     hipEvent_t chunk_done[BHRT_MAX_CHUNKS], chunk_copied[BHRT_MAX_CHUNKS];
+    /* busy span of the trace kernels since the last stats reset: span_ref is recorded before
+     * the first launch; [span_lo, span_hi] = earliest start / latest end relative to it (ms).
+     * With launches overlapping on several streams, span / launches is the GPU time per
+     * launch that the per-launch HIP-event durations (which overlap) cannot give. */
+    hipEvent_t span_ref;
+    int span_on;
+    double span_lo, span_hi;
 } devctx_t;
 
 static _Thread_local devctx_t* g_ctx[BHRT_MAX_DEV];
@@ -169,6 +176,11 @@ static devctx_t* ctx_get(int device) {
         hipMalloc((void**)&c->d_ctl, BHRT_RING * BHRT_CTL_WORDS * sizeof(unsigned long long)) !=
             hipSuccess) {
         set_err("cannot create HIP stream / control blocks on device %d", device);
+        free(c);
+        return NULL;
+    }
+    if (hipEventCreate(&c->span_ref) != hipSuccess) {
+        set_err("hipEventCreate failed");
         free(c);
         return NULL;
     }
@@ -248,8 +260,12 @@ static int harvest(devctx_t* c) {
     for (int i = 0; i < c->npend; i++) HIP_TRY(hipEventSynchronize(c->pend[i].ev1));
     HIP_TRY(hipMemcpy(h, c->d_ctl, sizeof h, hipMemcpyDeviceToHost));
     for (int i = 0; i < c->npend; i++) {
-        float ms = 0.f;
+        float ms = 0.f, t0 = 0.f, t1 = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, c->pend[i].ev0, c->pend[i].ev1));
+        HIP_TRY(hipEventElapsedTime(&t0, c->span_ref, c->pend[i].ev0));
+        HIP_TRY(hipEventElapsedTime(&t1, c->span_ref, c->pend[i].ev1));
+        if (t0 < c->span_lo) c->span_lo = t0;
+        if (t1 > c->span_hi) c->span_hi = t1;
         const unsigned long long* w = h + c->pend[i].slot * BHRT_CTL_WORDS;
         g_stats.rays += w[1];
         g_stats.iterations += w[2];
@@ -266,8 +282,15 @@ static int harvest(devctx_t* c) {
 
 int bhrt_get_stats(bhrt_stats* out, int reset) {
     int rc = 0;
-    for (int d = 0; d < BHRT_MAX_DEV; d++)
-        if (g_ctx[d] && harvest(g_ctx[d]) != 0) rc = -1;
+    double span = 0.0;
+    for (int d = 0; d < BHRT_MAX_DEV; d++) {
+        devctx_t* c = g_ctx[d];
+        if (!c) continue;
+        if (harvest(c) != 0) rc = -1;
+        if (c->span_on && c->span_hi > c->span_lo) span += c->span_hi - c->span_lo;
+        if (reset) c->span_on = 0;
+    }
+    g_stats.span_ms = span;
     if (out) *out = g_stats;
     if (reset) memset(&g_stats, 0, sizeof g_stats);
     return rc;
@@ -405,6 +428,12 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
     kp->ctl = c->d_ctl + (size_t)slot * BHRT_CTL_WORDS;
     HIP_TRY(hipMemsetAsync(kp->ctl, 0, BHRT_CTL_WORDS * sizeof(unsigned long long), stream));
+    if (!c->span_on) {
+        HIP_TRY(hipEventRecord(c->span_ref, stream));
+        c->span_on = 1;
+        c->span_lo = 1e300;
+        c->span_hi = -1e300;
+    }
     pending_t* p = &c->pend[c->npend];
     p->slot = slot;
     p->ev0 = c->evpool[2 * c->npend];

@@ -66,6 +66,14 @@ struct Counters {
 // advances of y1, y2, y3) lanes and waves whose |delta| exceeds 0.05 / 0.1 / 0.2 / pi/4,
 // plus lane occupancy of the persistent loop. Never part of the product build.
 __device__ unsigned long long g_dstats[BHRT_STATS_N];
+// per wave of the hot k_trace launch: s_memrealtime (100 MHz) at start, when the queue was
+// first seen exhausted, and at exit (tail analysis, tools/wave_tail.py)
+#define BHRT_WAVE_T_MAX 16384
+__device__ unsigned long long g_wave_t[3 * BHRT_WAVE_T_MAX];
+__device__ unsigned g_wave_n;
+// lane-iterations and wave passes per 250 us of a wave's run time (throughput over time)
+#define BHRT_TBINS 128
+__device__ unsigned long long g_tbins[2 * BHRT_TBINS];
 __device__ __forceinline__ void dstat(Counters& n, int site, double delta) {
     const double thr[4] = {0.05, 0.1, 0.2, 0.78539816339744828};
     const unsigned long long act = __ballot(1);
@@ -990,6 +998,12 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     int rid = 0;
     bool live = false;
     bool exhausted = false;  // wave-uniform
+#if BHRT_STATS
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_exh = 0;
+    int tbin = 0;
+    unsigned long long tb_lanes = 0, tb_passes = 0;
+#endif
     for (;;) {
         const unsigned long long live_mask = __ballot(live);
         int n_live = __popcll(live_mask);
@@ -999,6 +1013,9 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             if (lane == 0) base = atomicAdd(head, (unsigned long long)need);
             base = __shfl(base, 0);
             exhausted = base + (unsigned long long)need >= total;
+#if BHRT_STATS
+            if (exhausted) t_exh = __builtin_amdgcn_s_memrealtime();
+#endif
             if (!live) {
                 const unsigned long long id = base + __popcll(~live_mask & below);
                 if (id < total) {
@@ -1022,6 +1039,20 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         if (lane == 0) {
             n.ds[60]++;
             n.ds[61] += n_live;
+            if (exhausted) {  // the tail: passes and live lanes after the queue ran dry
+                n.ds[62]++;
+                n.ds[63] += n_live;
+            }
+            const int b = min((int)((__builtin_amdgcn_s_memrealtime() - t_start) / 25000ull),
+                              BHRT_TBINS - 1);
+            if (b != tbin) {
+                atomicAdd(&g_tbins[2 * tbin], tb_lanes);
+                atomicAdd(&g_tbins[2 * tbin + 1], tb_passes);
+                tbin = b;
+                tb_lanes = tb_passes = 0;
+            }
+            tb_lanes += n_live;
+            tb_passes++;
         }
 #endif
         if (live) {
@@ -1062,6 +1093,17 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     for (int j = 0; j < BHRT_STATS_N; j++) {
         const unsigned long long v = wave_sum(n.ds[j]);
         if (lane == 0 && v) atomicAdd(&g_dstats[j], v);
+    }
+    if (!HUGE && lane == 0) {
+        atomicAdd(&g_tbins[2 * tbin], tb_lanes);
+        atomicAdd(&g_tbins[2 * tbin + 1], tb_passes);
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        const unsigned w = atomicAdd(&g_wave_n, 1u);
+        if (w < BHRT_WAVE_T_MAX) {
+            g_wave_t[3 * w] = t_start;
+            g_wave_t[3 * w + 1] = t_exh;
+            g_wave_t[3 * w + 2] = t_end;
+        }
     }
 #endif
 }
@@ -1294,6 +1336,37 @@ extern "C" __attribute__((visibility("default"))) int bhrt_debug_stats(unsigned 
         rc = (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dstats), zero, sizeof(zero));
     }
     return rc;
+}
+
+// Per-wave (start, queue-exhausted, end) s_memrealtime stamps of the hot k_trace launches
+// since the last reset; returns the number of waves recorded (<= max), or -1.
+extern "C" __attribute__((visibility("default"))) int bhrt_debug_wave_times(
+    unsigned long long* out, int max, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    unsigned n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_wave_n), sizeof(n)) != hipSuccess) return -1;
+    if (n > BHRT_WAVE_T_MAX) n = BHRT_WAVE_T_MAX;
+    if ((int)n > max) n = (unsigned)max;
+    if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), 3 * sizeof(unsigned long long) * n) !=
+                 hipSuccess)
+        return -1;
+    if (reset) {
+        const unsigned zero = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_n), &zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return (int)n;
+}
+
+// [2 * BHRT_TBINS] (lane-iterations, wave passes) per 250 us bin of wave run time
+extern "C" __attribute__((visibility("default"))) int bhrt_debug_time_bins(
+    unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbins), sizeof(g_tbins)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long zero[2 * BHRT_TBINS] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tbins), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return BHRT_TBINS;
 }
 #endif
 
