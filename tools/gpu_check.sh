@@ -14,4 +14,6 @@ rc=$?
 echo "exit=$rc"
 tail -3 $OUT/smoke.log $OUT/pytest_gpu.log 2>/dev/null
 cat $OUT/bench.json 2>/dev/null
+# per-launch GPU time of the overlapping trace launches in the kernel trace (warm-up skipped)
+python tools/trace_span.py $(find $OUT/prof -name "*kernel_trace.csv" | head -1) --skip 1 2>/dev/null
 exit $rc
