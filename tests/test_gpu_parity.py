@@ -237,6 +237,35 @@ def test_device_api_on_torch_stream(bhrt_lib):
     assert counts.sum().item() == W * H
 
 
+@pytest.mark.parametrize("cname", ["C1", "C4"])
+def test_overlapping_frames_on_two_streams(bhrt_lib, cname):
+    """bench.py's pipelined mode: consecutive frames on alternating streams, in flight together
+    (launch scratch is per stream), each equal to a lone render; span_ms covers the launches."""
+    import torch
+    c = configs.CONFIGS[cname]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera("B")
+    W, H = (c.width, c.height) if cname == "C1" else (640, 360)
+    ref = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs = [{f: torch.full((W * H,), -1, dtype=torch.int32 if f in ("result", "steps")
+                           else torch.float64, device="cuda") for f in abi.SOA_FIELDS}
+            for _ in range(4)]
+    torch.cuda.synchronize()
+    bhrt_lib.stats(reset=True)
+    for k, t in enumerate(bufs):
+        s = streams[k % 2]
+        bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                     bhrt_lib.soa_from_tensors(t), s.cuda_stream)
+    torch.cuda.synchronize()
+    st = bhrt_lib.stats(reset=True)
+    assert st["launches"] == 4 and st["rays"] == 4 * W * H
+    assert st["span_ms"] > 0.0
+    for t in bufs:
+        for f in abi.SOA_FIELDS:
+            assert np.array_equal(t[f].cpu().numpy(), ref[f], equal_nan=True), f
+
+
 @pytest.mark.parametrize("cname", ["C2", "C4", "C5"])
 def test_refill_threshold_does_not_change_results(bhrt_lib, cname):
     """The wave refill policy (0 = the per-scene default) is a speed knob only."""
