@@ -270,6 +270,26 @@ __device__ __forceinline__ bool sincos_shift_wide(double a, double s0, double c0
 #ifndef BHRT_SHIFT_FMA2
 #define BHRT_SHIFT_FMA2 1
 #endif
+// The short-interval shift alone (BHRT_SHORT_SHIFT's polynomials); returns true when
+// |x - a| > 1/16, i.e. when the caller must redo s, c with sincos_shift_wide / bhrt_sincos.
+__device__ __forceinline__ __attribute__((unused)) bool short_shift(double a, double s0, double c0, double x, double& s,
+                                            double& c) {
+    const double delta = x - a;
+    constexpr double S1 = -0.16666666666662605, S2 = 0.00833333327878775,
+                     S3 = -0.00019839069723619096;
+    constexpr double C1 = 0.04166666666666157, C2 = -0.0013888888827212717,
+                     C3 = 2.479927034006378e-05;
+    const double z = delta * delta;
+    const double sd = delta + (z * delta) * fmac_k(z, fmac_k(z, S3, S2), S1);
+    const double cm1 = z * __builtin_fma(z, fmac_k(z, fmac_k(z, C3, C2), C1), -0.5);
+    s = __builtin_fma(c0, sd, __builtin_fma(s0, cm1, s0));
+    c = __builtin_fma(-s0, sd, __builtin_fma(c0, cm1, c0));
+    return !(fabs(delta) <= 0.0625);
+}
+#ifndef BHRT_ADV_MERGE
+#define BHRT_ADV_MERGE 0
+#endif
+
 __device__ __forceinline__ void shift_or_eval(double a, double s0, double c0, double x, double& s,
                                               double& c, Counters* hc) {
 #if BHRT_SHORT_SHIFT
@@ -331,6 +351,9 @@ struct Trig1 {
 #endif
 #ifndef BHRT_TEST_D012
 #define BHRT_TEST_D012 0
+#endif
+#ifndef BHRT_CLAMP_IN_PLAIN
+#define BHRT_CLAMP_IN_PLAIN 1
 #endif
 // ray_derivatives' a = 0 accelerations in the literal form (:92-130, evaluation order as
 // written, divisions as div_nr / IEEE), from sin, cos of the unclamped theta.
@@ -430,8 +453,14 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         // clamp. A lane whose result is not a plain |d| <= 10 value (never on a C2 frame)
         // recomputes it in the literal form before the repair and clamps.
         const double rc = max_raw(y[0], sc.rs_x1_5);
+#if BHRT_CLAMP_IN_PLAIN
+        // the |sin theta| >= 0.01 clamp of :110-114 never binds on the fast path: a lane where
+        // it would takes the literal form below (never on a C2 frame)
+        const double sc_ = st;
+#else
         double sc_ = st;
         if (fabs(st) < 0.01) sc_ = (st >= 0.0) ? 0.01 : -0.01;
+#endif
 #if BHRT_ONE_RCP
         // 1/r and 1/sin theta from one reciprocal of the product (r sin theta in [0.03, 1e150])
         const double w = rcp_nr(rc * sc_);
@@ -446,7 +475,11 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         d[4] = __builtin_fma(p * -2.0, y[4], u * (ct * y[5]));
         d[5] = (y[5] * -2.0) * __builtin_fma(y[4], ct * ys, p);
         const int plain = (int)(rc < 1.0e150) & (int)(fabs(d[3]) <= 10.0) &
-                          (int)(fabs(d[4]) <= 10.0) & (int)(fabs(d[5]) <= 10.0);
+                          (int)(fabs(d[4]) <= 10.0) & (int)(fabs(d[5]) <= 10.0)
+#if BHRT_CLAMP_IN_PLAIN
+                          & (int)(fabs(st) >= 0.01)
+#endif
+            ;
         if (__builtin_expect(plain, 1)) return;
         accel_literal(y, d, sc, st, ct);
         repair_clamp(d);
@@ -595,7 +628,7 @@ __device__ __forceinline__ void sph2cart_t(double r, double st, double ct, doubl
 // sin, cos of x from those of a, the same component one iteration earlier:
 // exact shift when sincos_shift's preconditions hold, direct evaluation otherwise. Per ray
 // only (never dependent on which wave runs the ray), so results stay reproducible.
-__device__ __forceinline__ void trig_advance(double a, double x, double& s, double& c,
+__device__ __forceinline__ __attribute__((unused)) void trig_advance(double a, double x, double& s, double& c,
                                              Counters* hc) {
     double s1, c1;
     shift_or_eval(a, s, c, x, s1, c1, hc);
@@ -783,10 +816,17 @@ __device__ __forceinline__ bool disk_test(Ray_& R, double nx, double ny, double 
 
 enum Term : int { T_NONE = 0, T_HORIZON, T_DISK, T_MAXDIST, T_MAXSTEPS };
 
+struct HSel {  // the four step sizes of the schedule, hoisted out of the kernel argument block
+    double far_, r15, r5, r2_5;
+};
+#ifndef BHRT_H_LOCAL
+#define BHRT_H_LOCAL 1
+#endif
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
 // on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
 template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE>
-__device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n) {
+__device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n,
+                                           const HSel* hs = nullptr) {
     Counters* const hc = HUGE ? nullptr : &n;
     // :543-548. One test of the sum (non-finite if any component is, or on overflow);
     // the per-component repair runs only then.
@@ -800,10 +840,18 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     }
     // step schedule (:556-571), written as selects so the first true test wins
     const double r = R.y[1];
-    double h = sc.h_far;
-    h = (r < sc.rs_x15) ? sc.h_15 : h;
-    h = (r < sc.rs_x5) ? sc.h_5 : h;
-    h = (r < sc.rs_x2_5) ? sc.h_2_5 : h;  // fmin(h, 0.1) is folded into the four values (host)
+    double h;
+    if (hs) {
+        h = hs->far_;
+        h = (r < sc.rs_x15) ? hs->r15 : h;
+        h = (r < sc.rs_x5) ? hs->r5 : h;
+        h = (r < sc.rs_x2_5) ? hs->r2_5 : h;
+    } else {
+        h = sc.h_far;
+        h = (r < sc.rs_x15) ? sc.h_15 : h;
+        h = (r < sc.rs_x5) ? sc.h_5 : h;
+        h = (r < sc.rs_x2_5) ? sc.h_2_5 : h;  // fmin(h, 0.1) is folded into the values (host)
+    }
     bool moved = true;
     if (METHOD != INTEGRATOR_RK4) n.iters++;  // RK4: counted at termination (k_trace)
     Trig1 tr;
@@ -828,9 +876,27 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
         dstat(n, 4, R.y[2] - a2);
         dstat(n, 5, R.y[3] - a3);
 #endif
+#if BHRT_ADV_MERGE && BHRT_SHORT_SHIFT
+        // the three advances' short shifts straight-line, then ONE rare-lane branch for any
+        // whose step left |delta| <= 1/16 (same per-lane results as three shift_or_eval calls)
+        double ns1, nc1, ns2, nc2, ns3, nc3;
+        const bool w1 = short_shift(tr.a, R.s1, R.c1, R.y[1], ns1, nc1);
+        const bool w2 = short_shift(a2, R.s2, R.c2, R.y[2], ns2, nc2);
+        const bool w3 = short_shift(a3, R.s3, R.c3, R.y[3], ns3, nc3);
+        if (__builtin_expect(w1 | w2 | w3, 0)) {
+            if (w1 && !sincos_shift_wide(tr.a, R.s1, R.c1, R.y[1], ns1, nc1))
+                bhrt_sincos(R.y[1], &ns1, &nc1, hc);
+            if (w2 && !sincos_shift_wide(a2, R.s2, R.c2, R.y[2], ns2, nc2))
+                bhrt_sincos(R.y[2], &ns2, &nc2, hc);
+            if (w3 && !sincos_shift_wide(a3, R.s3, R.c3, R.y[3], ns3, nc3))
+                bhrt_sincos(R.y[3], &ns3, &nc3, hc);
+        }
+        R.s1 = ns1; R.c1 = nc1; R.s2 = ns2; R.c2 = nc2; R.s3 = ns3; R.c3 = nc3;
+#else
         trig_advance(tr.a, R.y[1], R.s1, R.c1, hc);
         trig_advance(a2, R.y[2], R.s2, R.c2, hc);
         trig_advance(a3, R.y[3], R.s3, R.c3, hc);
+#endif
     }
     sph2cart_t(R.y[1], R.s2, R.c2, R.s3, R.c3, x, y, z);
 #else
@@ -866,8 +932,11 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
 }
 
 // fill_hit_info (raytracer.c:299-333) / the disk branch of trace_ray (:728-753)
+// sky_tab: the init table's (thetadot, phidot) rows (k_trace with BHRT_SKY_RELOAD, which keeps
+// these two per-ray constants out of registers), or NULL to use R.y6, R.y7.
 __device__ __forceinline__ void store_hit(const bhrt_frame_soa& s, int i, const Ray_& R,
-                                          int term, const Scene& sc) {
+                                          int term, const Scene& sc,
+                                          const double* sky_tab = nullptr, long n = 0) {
     int result, steps;
     double hx, hy, hz, tdil, sx = 0.0, sy = 0.0, sz = 0.0;
     if (term == T_DISK) {
@@ -885,7 +954,10 @@ __device__ __forceinline__ void store_hit(const bhrt_frame_soa& s, int i, const 
         hy = R.py;
         hz = R.pz;
         tdil = 1.0 / sqrt(1.0 - sc.rs / R.y[1]);
-        if (term == T_MAXDIST) normalize3(R.y[5], R.y6, R.y7, sx, sy, sz);  // state[5..7]
+        if (term == T_MAXDIST) {  // state[5..7]
+            const double y6 = sky_tab ? sky_tab[i] : R.y6, y7 = sky_tab ? sky_tab[n + i] : R.y7;
+            normalize3(R.y[5], y6, y7, sx, sy, sz);
+        }
     }
     if (s.result) s.result[i] = result;
     if (s.steps) s.steps[i] = steps;
@@ -899,13 +971,23 @@ __device__ __forceinline__ void store_hit(const bhrt_frame_soa& s, int i, const 
     if (s.sky_z) s.sky_z[i] = sz;
 }
 
+#ifndef BHRT_SKY_RELOAD
+#define BHRT_SKY_RELOAD 0
+#endif
+#if BHRT_SKY_RELOAD
+#define SKY_TAB(kp) ((kp).init + 6 * (long)(kp).n)
+#else
+#define SKY_TAB(kp) nullptr
+#endif
 __device__ __forceinline__ void load_init(const bhrt_kparams& kp, int i, Ray_& R) {
     const double* f = kp.init;
     const long n = kp.n;
 #pragma unroll
     for (int j = 0; j < 6; j++) R.y[j] = f[j * n + i];
+#if !BHRT_SKY_RELOAD
     R.y6 = f[6 * n + i];
     R.y7 = f[7 * n + i];
+#endif
     R.dx = f[8 * n + i];
     R.dy = f[9 * n + i];
     R.dz = f[10 * n + i];
@@ -998,6 +1080,9 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     int rid = 0;
     bool live = false;
     bool exhausted = false;  // wave-uniform
+#if BHRT_H_LOCAL
+    const HSel hsel{kp.sc.h_far, kp.sc.h_15, kp.sc.h_5, kp.sc.h_2_5};
+#endif
 #if BHRT_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_exh = 0;
@@ -1024,7 +1109,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
-                        store_hit(kp.out, rid, R, T_MAXSTEPS, kp.sc);
+                        store_hit(kp.out, rid, R, T_MAXSTEPS, kp.sc, SKY_TAB(kp), kp.n);
                         live = false;
                     }
                 }
@@ -1056,7 +1141,11 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         }
 #endif
         if (live) {
+#if BHRT_H_LOCAL
+            const int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, &hsel);
+#else
             const int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n);
+#endif
             if (METHOD == INTEGRATOR_RK4 && (term != T_NONE || (!HUGE && n.huge)))
                 n.iters += R.k;  // every RK4 iteration moves, so R.k = iterations executed
             if (!HUGE && n.huge) {  // hand the ray to the HUGE instantiation
@@ -1065,7 +1154,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 kp.redo[atomicAdd(kp.ctl + 6, 1ull)] = rid;
                 live = false;
             } else if (term != T_NONE) {
-                store_hit(kp.out, rid, R, term, kp.sc);
+                store_hit(kp.out, rid, R, term, kp.sc, SKY_TAB(kp), kp.n);
                 live = false;
             }
         }
