@@ -616,22 +616,42 @@ static int readback_issue(shard_job* j, const bhrt_frame_soa* host, char* stage,
     return 0;
 }
 
-/* copy a landed shard from `stage` into `host`, un-permuting cyclic row blocks */
+/* copy a landed shard from `stage` into `host`, un-permuting cyclic row blocks. A C2 frame
+ * is ~200 MB of fields; one thread copies it at a fraction of the host's memory bandwidth, so
+ * the rows of large shards are split over OpenMP threads (BHRT_HOST_THREADS, default 8). */
+static int host_threads(void) {
+    const char* e = getenv("BHRT_HOST_THREADS");
+    int t = e ? atoi(e) : 8;
+    return t < 1 ? 1 : (t > 64 ? 64 : t);
+}
+
 static void readback_finish(const shard_job* j, const bhrt_frame_soa* host, const char* stage,
                             int W, const bhrt_rows* rows) {
+    const int nthreads = host_threads();
+    const int big = (size_t)j->n * 8 >= ((size_t)1 << 22); /* >= 4 MB per double field */
+    const int permute = rows && rows->num_shards > 1 && W > 0;
     size_t off = 0;
     for (int f = 0; f < BHRT_NFIELDS; f++) {
         if (!WANTED(j, host, f)) continue;
         char* dst = (char*)*soa_slot((bhrt_frame_soa*)host, f);
-        size_t fs = k_fsize[f];
-        if (!rows || rows->num_shards <= 1) {
-            memcpy(dst, stage + off, fs * (size_t)j->n);
-        } else {
-            long nrow = j->n / W;
+        const char* src = stage + off;
+        const size_t fs = k_fsize[f];
+        if (permute) { /* whole rows; local row r is image row g */
+            const size_t row_bytes = fs * (size_t)W;
+            const long nrow = j->n / W, B = rows->row_block, S = rows->num_shards,
+                       sh = rows->shard;
+#pragma omp parallel for schedule(static) num_threads(nthreads) if (big)
             for (long r = 0; r < nrow; r++) {
-                long B = rows->row_block;
-                long g = ((r / B) * rows->num_shards + rows->shard) * B + r % B;
-                memcpy(dst + fs * (size_t)(g * W), stage + off + fs * (size_t)(r * W), fs * (size_t)W);
+                const long g = ((r / B) * S + sh) * B + r % B;
+                memcpy(dst + row_bytes * (size_t)g, src + row_bytes * (size_t)r, row_bytes);
+            }
+        } else { /* one contiguous block, copied in pieces */
+            const size_t total = fs * (size_t)j->n, piece = (size_t)1 << 20;
+            const long npieces = (long)((total + piece - 1) / piece);
+#pragma omp parallel for schedule(static) num_threads(nthreads) if (big)
+            for (long q = 0; q < npieces; q++) {
+                const size_t a = piece * (size_t)q, len = total - a < piece ? total - a : piece;
+                memcpy(dst + a, src + a, len);
             }
         }
         off += fs * (size_t)j->n;
@@ -670,7 +690,7 @@ int bhrt_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* dk,
     const int block = 8;
     if (ndev > 1 && H < ndev * block) ndev = 1;
     const long per_dev = (long)W * H / ndev;  /* chunks per device: */
-    int K = per_dev >= (1L << 21) ? 8 : (per_dev >= (1L << 18) ? 4 : 1);
+    int K = per_dev >= (1L << 20) ? 8 : (per_dev >= (1L << 18) ? 4 : 1);
     if (H < K * ndev * block) K = 1;
     const char* env = getenv("BHRT_HOST_CHUNKS");
     if (env && atoi(env) >= 1 && atoi(env) <= BHRT_MAX_CHUNKS && H >= atoi(env) * ndev * block)
