@@ -1067,12 +1067,23 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 // HUGE = false: the hot instantiation, rays [0, kp.n) from queue head ctl[0]. A ray that
 // needs a large-argument sincos (bhrt_sincos) is dropped and its id appended to kp.redo
 // (count ctl[6]). HUGE = true: re-traces kp.redo[0, ctl[6]) from queue head ctl[7].
-template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE>
+// INL: camera launch whose rays are set up here, at refill (ray_init_camera), instead of
+// being loaded from k_init's 168-byte table: used where rays are short-lived (Kerr, RKF45), so
+// refills are frequent and each table load stalls its wave on HBM latency.
+// The sin/cos anchors of the shared origin are the same for every ray: computed once per wave.
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, bool INL = false>
 __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     unsigned long long* const head = HUGE ? kp.ctl + 7 : kp.ctl;
     const unsigned long long total =
         HUGE ? *(volatile unsigned long long*)(kp.ctl + 6) : (unsigned long long)kp.n;
     if (total == 0) return;
+    double as1 = 0.0, ac1 = 0.0, as2 = 0.0, ac2 = 0.0, as3 = 0.0, ac3 = 0.0;
+    if (INL) {  // trig_anchor of the origin state (r0, th0, ph0); the host keeps |r0| < 2^20
+        Counters dummy;
+        bhrt_sincos(kp.cam.r0, &as1, &ac1, &dummy);
+        bhrt_sincos(kp.cam.th0, &as2, &ac2, &dummy);
+        bhrt_sincos(kp.cam.ph0, &as3, &ac3, &dummy);
+    }
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
     Counters n;
@@ -1105,7 +1116,17 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 const unsigned long long id = base + __popcll(~live_mask & below);
                 if (id < total) {
                     rid = HUGE ? kp.redo[id] : (int)id;
-                    load_init(kp, rid, R);
+                    if (INL) {
+                        ray_init_camera(R, kp.cam, rid);
+                        R.s1 = as1;
+                        R.c1 = ac1;
+                        R.s2 = as2;
+                        R.c2 = ac2;
+                        R.s3 = as3;
+                        R.c3 = ac3;
+                    } else {
+                        load_init(kp, rid, R);
+                    }
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
@@ -1338,29 +1359,53 @@ int grid_for(const void* fn, int n) {
     return blocks < 1 ? 1 : (int)blocks;
 }
 
-template <int METHOD, bool DISK, bool SPIN0, bool FAR>
-int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool INL>
+void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     static int grid_cap = 0, grid_huge = 0;  // resident workgroups per instantiation
     if (grid_cap == 0) {
         grid_cap = grid_for(
-            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, false>), 1 << 30);
+            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, false, INL>), 1 << 30);
         grid_huge = grid_for(
-            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, true>), 1 << 30);
+            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, true, INL>), 1 << 30);
     }
-    if (kp.src == BHRT_SRC_CAMERA)
+    int blocks = (kp.n + 255) / 256;
+    if (blocks > grid_cap) blocks = grid_cap;
+    if (blocks < 1) blocks = 1;
+    k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, 256, 0, st>>>(kp);
+    // rays evicted by the large-argument check (normally none: every wave exits at once)
+    k_trace<METHOD, DISK, SPIN0, FAR, true, INL><<<blocks < grid_huge ? blocks : grid_huge, 256,
+                                                   0, st>>>(kp);
+}
+
+#ifndef BHRT_INLINE_CAMERA
+#define BHRT_INLINE_CAMERA 1
+#endif
+template <int METHOD, bool DISK, bool SPIN0, bool FAR>
+int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    // camera rays set up inside k_trace where rays are short-lived: scenes with a disk (most
+    // rays end on it within tens of iterations: C4 +6.6%, C3 +16.5%) except the a = 0 RK4 path
+    // (C2: lifetimes up to max_steps, refills rare; the set-up code would cost that kernel its
+    // third wave per SIMD). Without a disk (C5: rays run ~40 RKF45 attempts to max_distance)
+    // it measured 5% slower (profiles/r01_ab_v10.txt).
+    constexpr bool CAN_INL = BHRT_INLINE_CAMERA && DISK && !(METHOD == INTEGRATOR_RK4 && SPIN0);
+    const bool inl = CAN_INL && kp.src == BHRT_SRC_CAMERA && fabs(kp.cam.r0) < 1048576.0;
+    if (inl)
+        ;
+    else if (kp.src == BHRT_SRC_CAMERA)
         k_init<BHRT_SRC_CAMERA><<<grid_for(reinterpret_cast<const void*>(&k_init<BHRT_SRC_CAMERA>),
                                            kp.n), 256, 0, st>>>(kp);
     else
         k_init<BHRT_SRC_RAYS><<<grid_for(reinterpret_cast<const void*>(&k_init<BHRT_SRC_RAYS>),
                                          kp.n), 256, 0, st>>>(kp);
-    int blocks = (kp.n + 255) / 256;
-    if (blocks > grid_cap) blocks = grid_cap;
-    if (blocks < 1) blocks = 1;
     if (ev0) (void)hipEventRecord(ev0, st);
-    k_trace<METHOD, DISK, SPIN0, FAR, false><<<blocks, 256, 0, st>>>(kp);
-    // rays evicted by the large-argument check (normally none: every wave exits at once)
-    k_trace<METHOD, DISK, SPIN0, FAR, true><<<blocks < grid_huge ? blocks : grid_huge, 256, 0,
-                                              st>>>(kp);
+    if constexpr (CAN_INL) {
+        if (inl)
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, true>(kp, st);
+        else
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, false>(kp, st);
+    } else {
+        launch_trace_pair<METHOD, DISK, SPIN0, FAR, false>(kp, st);
+    }
     if (ev1) (void)hipEventRecord(ev1, st);
     if (kp.out.rgb_r || kp.out.rgba32f || kp.out.rgba8) {
         if (kp.src == BHRT_SRC_CAMERA)
