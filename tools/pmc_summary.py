@@ -8,6 +8,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
@@ -17,7 +18,8 @@ for p in sorted(glob.glob(f"{src}/p*/pass_counter_collection.csv")):
     acc = collections.defaultdict(float)
     for row in csv.DictReader(open(p)):
         # the hot instantiation only (HUGE = false); the redo launch is normally empty
-        if not row.get("Kernel_Name", "").rstrip().endswith("false>(bhrt_kparams)"):
+        m = re.search(r"k_trace<([^>]*)>", row.get("Kernel_Name", ""))
+        if not m or m.group(1).split(",")[4].strip() != "false":   # template arg 5 = HUGE
             continue
         acc[(row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
     for (disp, name), v in acc.items():

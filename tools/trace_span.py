@@ -1,7 +1,7 @@
 """Per-launch GPU time of a kernel from a rocprofv3 kernel trace (CSV), for launches that
 overlap on several streams (bench.py --streams 2).
 
-  python tools/trace_span.py gpurun_out/prof/run_kernel_trace.csv [--kernel 'k_trace<0, true, true, false, false>']
+  python tools/trace_span.py gpurun_out/prof/run_kernel_trace.csv [--kernel 'k_trace<0, true, true, false, false, false>']
 
 Prints the number of dispatches, their mean start..end duration (what rocprofv3 --stats
 averages; overlapping launches double-count the overlap) and the union of their intervals
@@ -14,7 +14,7 @@ import csv
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--kernel", default="k_trace<0, true, true, false, false>")
+    ap.add_argument("--kernel", default="k_trace<0, true, true, false, false, false>")
     ap.add_argument("--skip", type=int, default=0, help="leave out the first k dispatches "
                     "(bench.py's untimed warm-up frames)")
     a = ap.parse_args()
