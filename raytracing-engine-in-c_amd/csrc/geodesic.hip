@@ -1056,11 +1056,29 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 #ifndef BHRT_WAVES_PER_EU
 #define BHRT_WAVES_PER_EU 0
 #endif
-#if BHRT_WAVES_PER_EU > 0
-#define BHRT_TRACE_BOUNDS __launch_bounds__(256, BHRT_WAVES_PER_EU)
-#else
-#define BHRT_TRACE_BOUNDS __launch_bounds__(256)
+// Per-instantiation occupancy target (waves per SIMD; 0 = the compiler's choice). Only
+// instantiations whose register peak sits just above a wave boundary get one:
+// BHRT_W_RKF45_DISK (RKF45, a = 0, disk: C3; 200 VGPRs = 2 waves by default) and
+// BHRT_W_RKF45_KERR (RKF45, a != 0, no disk: C5; 104 VGPRs = 4 waves).
+#ifndef BHRT_W_RKF45_DISK
+#define BHRT_W_RKF45_DISK 0
 #endif
+#ifndef BHRT_W_RKF45_KERR
+#define BHRT_W_RKF45_KERR 6
+#endif
+#ifndef BHRT_W_RK4_KERR_DISK
+#define BHRT_W_RK4_KERR_DISK 0
+#endif
+template <int METHOD, bool DISK, bool SPIN0>
+constexpr int trace_waves() {
+    return BHRT_WAVES_PER_EU > 0 ? BHRT_WAVES_PER_EU
+         : (METHOD == INTEGRATOR_RKF45 && DISK && SPIN0) ? BHRT_W_RKF45_DISK
+         : (METHOD == INTEGRATOR_RKF45 && !DISK && !SPIN0) ? BHRT_W_RKF45_KERR
+         : (METHOD == INTEGRATOR_RK4 && DISK && !SPIN0) ? BHRT_W_RK4_KERR_DISK
+         : 0;
+}
+#define BHRT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, 256), \
+                                         amdgpu_waves_per_eu(trace_waves<METHOD, DISK, SPIN0>() > 0 ? trace_waves<METHOD, DISK, SPIN0>() : 1)))
 
 // FAR: some ray may take ray_derivatives' weak-field branch (origin beyond 15 rs). A camera
 // frame knows this once for all its rays (shared origin); ray arrays always assume it.
