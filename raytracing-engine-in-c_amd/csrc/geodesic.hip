@@ -664,8 +664,7 @@ struct Ray_ {
     double y[6];        // (t, r, theta, phi, tdot, rdot)
     double y6, y7;      // (thetadot, phidot): constants, see header
     double dx, dy, dz;  // Ray.direction as given (disk test)
-    double px, py, pz;  // current Cartesian position
-    double qx, qy, qz;  // disk hit point
+    double px, py, pz;  // current Cartesian position; the disk hit point once T_DISK
     double dist;
     double s1, c1, s2, c2, s3, c3;  // sin, cos of y[1], y[2], y[3] (BHRT_TRIG_CHAIN)
     int k;              // iterations executed
@@ -806,9 +805,11 @@ __device__ __forceinline__ bool disk_test(Ray_& R, double nx, double ny, double 
     const double qx = R.px + R.dx * t, qy = R.py + R.dy * t, qz = R.pz + R.dz * t;
     const double s = qx * qx + qy * qy;
     if (s >= sc.disk_in_sq && s <= sc.disk_out_sq) {
-        R.qx = qx;
-        R.qy = qy;
-        R.qz = qz;
+        // the ray ends here: the hit point replaces the current point, so no extra
+        // loop-carried registers hold it (the caller reads it from R.px..pz; +0.9% on C2)
+        R.px = qx;
+        R.py = qy;
+        R.pz = qz;
         return true;
     }
     return false;
@@ -910,7 +911,7 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     R.k++;
     // segment k = (p_k, p_{k-1}) is stored and scanned by trace_ray iff k < max_steps
     if (DISK && R.k < sc.max_steps && disk_test(R, ox, oy, oz, sc)) {
-        R.dist += len3(R.qx - ox, R.qy - oy, R.qz - oz);
+        R.dist += len3(R.px - ox, R.py - oy, R.pz - oz);
         return T_DISK;
     }
     if (R.y[1] <= sc.rs_x1_05) return T_HORIZON;
@@ -921,7 +922,7 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
         if (DISK && R.k + 1 < sc.max_steps && (x != ox || y != oy || z != oz) &&
             disk_test(R, x, y, z, sc)) {
             R.k++;
-            R.dist += len3(R.qx - x, R.qy - y, R.qz - z);
+            R.dist += len3(R.px - x, R.py - y, R.pz - z);
             return T_DISK;
         }
         R.k = sc.max_steps;
@@ -942,10 +943,10 @@ __device__ __forceinline__ void store_hit(const bhrt_frame_soa& s, int i, const 
     if (term == T_DISK) {
         result = RAY_DISK;
         steps = R.k;
-        hx = R.qx;
-        hy = R.qy;
-        hz = R.qz;
-        tdil = 1.0 / sqrt(1.0 - sc.rs / len3(R.qx, R.qy, R.qz));
+        hx = R.px;
+        hy = R.py;
+        hz = R.pz;
+        tdil = 1.0 / sqrt(1.0 - sc.rs / len3(R.px, R.py, R.pz));
     } else {
         result = term == T_HORIZON ? RAY_HORIZON
                                    : (term == T_MAXDIST ? RAY_MAX_DISTANCE : RAY_MAX_STEPS);
@@ -1056,10 +1057,17 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 #ifndef BHRT_WAVES_PER_EU
 #define BHRT_WAVES_PER_EU 0
 #endif
-// Per-instantiation occupancy target (waves per SIMD; 0 = the compiler's choice). Only
-// instantiations whose register peak sits just above a wave boundary get one:
-// BHRT_W_RKF45_DISK (RKF45, a = 0, disk: C3; 200 VGPRs = 2 waves by default) and
-// BHRT_W_RKF45_KERR (RKF45, a != 0, no disk: C5; 104 VGPRs = 4 waves).
+// Per-instantiation occupancy target (waves per SIMD; 0 = the compiler's choice), same-box
+// A/B in profiles/r01_ab_v11_occupancy.txt:
+//  * BHRT_W_RK4_A0 (RK4, a = 0: C1, C2) = 4. The straight-line iteration needs <= 123 VGPRs;
+//    the register peak (160) sits in the rare-lane blocks (literal accelerations, wide trig
+//    shifts, stores). Capped at 128 the allocator spills only inside those blocks -- the hot
+//    blocks are instruction-for-instruction the 3-wave code -- so C2 gains the 4th wave
+//    (+4.6%; C1 neutral).
+//  * BHRT_W_RKF45_KERR (RKF45, a != 0, no disk: C5) = 6 (104 VGPRs = 4 waves by default;
+//    6 waves +4%, 5 +2.6%, 7/8 slower).
+//  * C3 (RKF45 a = 0 disk, 200 VGPRs) and C4 (RK4 Kerr disk, 125) keep the compiler's
+//    choice: forcing one more wave spills in their hot blocks (-14%, -1.5%).
 #ifndef BHRT_W_RKF45_DISK
 #define BHRT_W_RKF45_DISK 0
 #endif
@@ -1069,12 +1077,16 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 #ifndef BHRT_W_RK4_KERR_DISK
 #define BHRT_W_RK4_KERR_DISK 0
 #endif
+#ifndef BHRT_W_RK4_A0
+#define BHRT_W_RK4_A0 4
+#endif
 template <int METHOD, bool DISK, bool SPIN0>
 constexpr int trace_waves() {
     return BHRT_WAVES_PER_EU > 0 ? BHRT_WAVES_PER_EU
          : (METHOD == INTEGRATOR_RKF45 && DISK && SPIN0) ? BHRT_W_RKF45_DISK
          : (METHOD == INTEGRATOR_RKF45 && !DISK && !SPIN0) ? BHRT_W_RKF45_KERR
          : (METHOD == INTEGRATOR_RK4 && DISK && !SPIN0) ? BHRT_W_RK4_KERR_DISK
+         : (METHOD == INTEGRATOR_RK4 && SPIN0) ? BHRT_W_RK4_A0
          : 0;
 }
 #define BHRT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, 256), \
@@ -1148,7 +1160,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
-                        store_hit(kp.out, rid, R, T_MAXSTEPS, kp.sc, SKY_TAB(kp), kp.n);
+                        store_hit(kp.out, rid, R, T_MAXSTEPS, kp.sc, INL ? nullptr : SKY_TAB(kp), kp.n);
                         live = false;
                     }
                 }
@@ -1193,7 +1205,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 kp.redo[atomicAdd(kp.ctl + 6, 1ull)] = rid;
                 live = false;
             } else if (term != T_NONE) {
-                store_hit(kp.out, rid, R, term, kp.sc, SKY_TAB(kp), kp.n);
+                store_hit(kp.out, rid, R, term, kp.sc, INL ? nullptr : SKY_TAB(kp), kp.n);
                 live = false;
             }
         }
