@@ -337,8 +337,11 @@ struct Trig1 {
 #ifndef BHRT_LAZY_CLAMP
 #define BHRT_LAZY_CLAMP 1
 #endif
+// 1/r and 1/sin(theta) from ONE reciprocal of r sin(theta): one v_rcp_f64 + refinement fewer
+// per stage, <= ~2 ulp instead of 1. Measured -6% at 3 waves/SIMD (v9, longer dependency
+// chain), +1.7% at 4 (v11, profiles/r01_ab_v11_occupancy.txt box 3).
 #ifndef BHRT_ONE_RCP
-#define BHRT_ONE_RCP 0
+#define BHRT_ONE_RCP 1
 #endif
 #ifndef BHRT_REASSOC
 #define BHRT_REASSOC 1

@@ -1,0 +1,30 @@
+"""Render one frame with the library in BHRT_LIB and save it (npz), or compare two saves:
+  BHRT_LIB=... python tools/diff_libs.py save C1 out.npz
+  python tools/diff_libs.py cmp a.npz b.npz
+Used to see how far an arithmetic variant moves the outputs (classes, steps, floats)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
+
+if sys.argv[1] == "save":
+    from bhrt import configs, lib
+    c = configs.CONFIGS[sys.argv[2]]
+    bh, dk, cfg = c.scene()
+    W, H = c.width, c.bench_height(1)
+    f = lib.render_frame(bh, dk, cfg, configs.camera("B"), W, H, c.method, c.flags)
+    np.savez(sys.argv[3], **f)
+else:
+    a, b = np.load(sys.argv[2]), np.load(sys.argv[3])
+    for k in a.files:
+        x, y = a[k], b[k]
+        same = np.sum((x == y) | (np.isnan(x) & np.isnan(y)) if x.dtype.kind == "f" else x == y)
+        msg = f"{k:14s} identical {same}/{x.size}"
+        if x.dtype.kind == "f":
+            ok = ~np.isnan(x) & ~np.isnan(y)
+            rel = np.abs(x[ok] - y[ok]) / np.maximum(np.abs(y[ok]), 1e-300)
+            msg += f"  max rel {rel.max() if rel.size else 0:.3e}"
+        print(msg)
