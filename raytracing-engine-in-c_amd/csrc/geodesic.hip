@@ -826,6 +826,38 @@ struct HSel {  // the four step sizes of the schedule, hoisted out of the kernel
 #ifndef BHRT_H_LOCAL
 #define BHRT_H_LOCAL 1
 #endif
+// :543-548, state NaN/Inf recovery at the top of every iteration. One test of the sum
+// (non-finite if any component is, or on overflow); the per-component repair runs only then.
+// ANCHOR = false: the caller knows state[1..3] are finite, so their sin/cos stay valid.
+template <bool ANCHOR = true>
+__device__ __forceinline__ void state_repair(Ray_& R, Counters* hc) {
+    if (__builtin_expect(
+            !isfinite(((R.y[0] + R.y[1]) + (R.y[2] + R.y[3])) + (R.y[4] + R.y[5])), 0)) {
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            if (!isfinite(R.y[i])) R.y[i] = (i < 4) ? 1.0 : 0.0;
+#if BHRT_TRIG_CHAIN
+        if (ANCHOR) trig_anchor(R, hc);
+#endif
+    }
+}
+// Where the loop-top recovery can only ever act on the first iteration, it runs once, at
+// refill (k_trace), and the hot loop drops its 6 VALU per iteration. That holds for RK4
+// without the far-field branch: every acceleration the loop feeds back is a plain |d| <= 10
+// value or comes out of the literal repair and clamps (zero on the Kerr branch), so from a
+// finite state a step adds at most h * 10 per stage to state[3..5] -- a finite double plus that
+// rounds to a finite double -- and h times a stage's state[3..5] (itself bounded by the
+// initial velocities, |v| < 2^512 for any finite set-up, plus 2 per step) to state[0..2],
+// which cannot reach 2^1024 within 2^31 steps. The far-field branch's 2M / r^2 is unclamped
+// and RKF45 keeps its k1 test, so those keep the per-iteration check (as does the HUGE redo).
+#ifndef BHRT_REPAIR_AT_REFILL
+#define BHRT_REPAIR_AT_REFILL 1
+#endif
+template <int METHOD, bool FAR, bool HUGE>
+constexpr bool repair_at_refill() {
+    return BHRT_REPAIR_AT_REFILL && METHOD == INTEGRATOR_RK4 && !FAR && !HUGE;
+}
+
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
 // on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
 template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE>
@@ -833,15 +865,9 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
                                            const HSel* hs = nullptr) {
     Counters* const hc = HUGE ? nullptr : &n;
     // :543-548. One test of the sum (non-finite if any component is, or on overflow);
-    // the per-component repair runs only then.
-    if (!isfinite(((R.y[0] + R.y[1]) + (R.y[2] + R.y[3])) + (R.y[4] + R.y[5]))) {
-#pragma unroll
-        for (int i = 0; i < 6; i++)
-            if (!isfinite(R.y[i])) R.y[i] = (i < 4) ? 1.0 : 0.0;
-#if BHRT_TRIG_CHAIN
-        trig_anchor(R, hc);
-#endif
-    }
+    // the per-component repair runs only then. Instantiations with repair_at_refill() run it
+    // once, when the ray is loaded: there a finite state stays finite (see state_repair).
+    if (!repair_at_refill<METHOD, FAR, HUGE>()) state_repair(R, hc);
     // step schedule (:556-571), written as selects so the first true test wins
     const double r = R.y[1];
     double h;
@@ -1160,6 +1186,11 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     } else {
                         load_init(kp, rid, R);
                     }
+                    // the first iteration's state recovery (the loop is skipped at max_steps <= 0);
+                    // an in-kernel camera set-up has a finite origin (|r0| < 2^20, host-checked),
+                    // so only the velocities can need it and the origin's sin/cos stay valid
+                    if (repair_at_refill<METHOD, FAR, HUGE>() && kp.sc.max_steps > 0)
+                        state_repair<!INL>(R, &n);
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
