@@ -512,6 +512,16 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
     repair_clamp(d);
 }
 
+// (see state_repair below)
+#ifndef BHRT_REPAIR_AT_REFILL
+#define BHRT_REPAIR_AT_REFILL 1
+#endif
+template <int METHOD, bool FAR, bool HUGE>
+constexpr bool repair_at_refill() {
+    return BHRT_REPAIR_AT_REFILL && (METHOD == INTEGRATOR_RK4 || METHOD == INTEGRATOR_RKF45) &&
+           !FAR && !HUGE;
+}
+
 // rk4_integrate (math_util.c:162-207) on the six live components; the running sum
 // ((k1 + 2k2) + 2k3) + k4 is the reference's left-to-right evaluation order.
 template <bool SPIN0, bool FAR, bool HUGE>
@@ -570,10 +580,12 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
                      d5 = -9.0 / 50.0, d6 = 2.0 / 55.0;
     double k1[6], k2[6], k3[6], k4[6], k5[6], k6[6], yt[6];
     rhs<SPIN0, FAR, HUGE>(y, k1, sc, far_ok, n, tr, true);
-    bool bad = false;
+    if (!repair_at_refill<INTEGRATOR_RKF45, FAR, HUGE>()) {
+        bool bad = false;
 #pragma unroll
-    for (int i = 0; i < 6; i++) bad |= !isfinite(k1[i]);  // :318-333
-    if (bad) return false;
+        for (int i = 0; i < 6; i++) bad |= !isfinite(k1[i]);  // :318-333
+        if (bad) return false;
+    }
     const double hb21 = h * b21;
 #pragma unroll
     for (int i = 0; i < 6; i++) yt[i] = y[i] + hb21 * k1[i];
@@ -842,21 +854,16 @@ __device__ __forceinline__ void state_repair(Ray_& R, Counters* hc) {
     }
 }
 // Where the loop-top recovery can only ever act on the first iteration, it runs once, at
-// refill (k_trace), and the hot loop drops its 6 VALU per iteration. That holds for RK4
-// without the far-field branch: every acceleration the loop feeds back is a plain |d| <= 10
-// value or comes out of the literal repair and clamps (zero on the Kerr branch), so from a
-// finite state a step adds at most h * 10 per stage to state[3..5] -- a finite double plus that
-// rounds to a finite double -- and h times a stage's state[3..5] (itself bounded by the
-// initial velocities, |v| < 2^512 for any finite set-up, plus 2 per step) to state[0..2],
-// which cannot reach 2^1024 within 2^31 steps. The far-field branch's 2M / r^2 is unclamped
-// and RKF45 keeps its k1 test, so those keep the per-iteration check (as does the HUGE redo).
-#ifndef BHRT_REPAIR_AT_REFILL
-#define BHRT_REPAIR_AT_REFILL 1
-#endif
-template <int METHOD, bool FAR, bool HUGE>
-constexpr bool repair_at_refill() {
-    return BHRT_REPAIR_AT_REFILL && METHOD == INTEGRATOR_RK4 && !FAR && !HUGE;
-}
+// refill (k_trace), and the hot loop drops its 6 VALU per iteration. That holds for RK4 and
+// RKF45 without the far-field branch: every acceleration the loop feeds back is a plain
+// |d| <= 10 value or comes out of the literal repair and clamps (zero on the Kerr branch), so
+// from a finite state a step adds at most h * 10 * (sum of |coefficients| <= 18) to
+// state[3..5] -- a finite double plus that rounds to a finite double -- and h times stage
+// values of state[3..5] (bounded by the initial velocities, |v| < 2^512 for any finite
+// set-up, plus 18 per step) to state[0..2], which cannot reach 2^1024 within 2^31 steps. For
+// the same reason RKF45's non-finite-k1 reject (math_util.c:318-333) can never fire there.
+// The far-field branch's 2M / r^2 is unclamped, so far-field instantiations keep both checks
+// every iteration (as does the HUGE redo).
 
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
 // on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
