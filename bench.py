@@ -56,7 +56,7 @@ FIELDS = abi.SOA_FIELDS
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", default="C2")
     p.add_argument("--camera", default="B")

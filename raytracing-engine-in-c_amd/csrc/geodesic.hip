@@ -1459,8 +1459,8 @@ template <int METHOD, bool DISK, bool SPIN0, bool FAR>
 int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     // camera rays set up inside k_trace where rays are short-lived: scenes with a disk (most
     // rays end on it within tens of iterations: C4 +6.6%, C3 +16.5%) except the a = 0 RK4 path
-    // (C2: lifetimes up to max_steps, refills rare; the set-up code would cost that kernel its
-    // third wave per SIMD). Without a disk (C5: rays run ~40 RKF45 attempts to max_distance)
+    // (C2: lifetimes up to max_steps, refills rare; in v10 the set-up code cost that kernel its
+    // third wave per SIMD, and since v11 its hot blocks must fit the 4-wave 128-VGPR cap). Without a disk (C5: rays run ~40 RKF45 attempts to max_distance)
     // it measured 5% slower (profiles/r01_ab_v10.txt).
     constexpr bool CAN_INL = BHRT_INLINE_CAMERA && DISK && !(METHOD == INTEGRATOR_RK4 && SPIN0);
     const bool inl = CAN_INL && kp.src == BHRT_SRC_CAMERA && fabs(kp.cam.r0) < 1048576.0;
