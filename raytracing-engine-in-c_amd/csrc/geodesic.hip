@@ -618,7 +618,16 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
         if (scale < kEps) scale = kEps;
         max_error = fmax(max_error, fabs(y5[i] - y4) / scale);
     }
-    if (max_error / sc.tol <= 1.0) {  // :402-434
+    // :402-434, RN(max_error / tol) <= 1. For a positive normal tol this is exactly
+    // max_error <= tol: x <= t gives x / t <= 1; x > t means x >= t + ulp(t), so x / t >=
+    // 1 + ulp(t) / t > 1 + 2^-53, the rounding midpoint above 1 (Inf and 0 agree too). The
+    // division stays for tol <= 0 or subnormal, where the two differ (wave-uniform branch).
+    bool accept;
+    if (sc.tol >= 2.2250738585072014e-308)
+        accept = max_error <= sc.tol;
+    else
+        accept = max_error / sc.tol <= 1.0;
+    if (accept) {
 #pragma unroll
         for (int i = 0; i < 6; i++) y[i] = y5[i];
         return true;
