@@ -609,24 +609,46 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
         yt[i] = y[i] + h * (b61 * k1[i] + b62 * k2[i] + b63 * k3[i] + b64 * k4[i] + b65 * k5[i]);
     rhs<SPIN0, FAR, HUGE>(yt, k6, sc, far_ok, n, tr, false);
     double y5[6];
-    double max_error = 0.0;
-#pragma unroll
-    for (int i = 0; i < 6; i++) {  // :367-391
-        const double y4 = y[i] + h * (c1 * k1[i] + c3 * k3[i] + c4 * k4[i] + c5 * k5[i]);
-        y5[i] = y[i] + h * (d1 * k1[i] + d3 * k3[i] + d4 * k4[i] + d5 * k5[i] + d6 * k6[i]);
-        double scale = fmax(fabs(y[i]), fabs(y5[i]));
-        if (scale < kEps) scale = kEps;
-        max_error = fmax(max_error, fabs(y5[i] - y4) / scale);
-    }
-    // :402-434, RN(max_error / tol) <= 1. For a positive normal tol this is exactly
-    // max_error <= tol: x <= t gives x / t <= 1; x > t means x >= t + ulp(t), so x / t >=
-    // 1 + ulp(t) / t > 1 + 2^-53, the rounding midpoint above 1 (Inf and 0 agree too). The
-    // division stays for tol <= 0 or subnormal, where the two differ (wave-uniform branch).
+    // :367-391 and :402-434: accept iff RN(max_i RN(|y5_i - y4_i| / scale_i) / tol) <= 1.
+    // For a positive normal tol the outer test is exactly max_error <= tol: x <= t gives
+    // x / t <= 1; x > t means x >= t + ulp(t), so x / t >= 1 + ulp(t) / t > 1 + 2^-53, the
+    // rounding midpoint above 1 (Inf and 0 agree too). That is, every component's RN(a / b)
+    // <= tol. Where the state is provably bounded (repair_at_refill: |b| < 2^600, so 1/b is
+    // normal) a component is decided from q = a * rcp(b), within 2^-50 of a / b: q < tol (1 -
+    // 2^-40) passes, q > tol (1 + 2^-40) rejects, and only a q inside that band (per lane, rare)
+    // takes the IEEE quotient. Other instantiations, and tol <= 0 or subnormal, keep the
+    // literal divisions (wave-uniform branch on tol).
+    constexpr bool FAST_NORM = repair_at_refill<INTEGRATOR_RKF45, FAR, HUGE>();
+    const bool tol_normal = sc.tol >= 2.2250738585072014e-308;
     bool accept;
-    if (sc.tol >= 2.2250738585072014e-308)
-        accept = max_error <= sc.tol;
-    else
-        accept = max_error / sc.tol <= 1.0;
+    if (FAST_NORM && tol_normal) {
+        const double lo = sc.tol * (1.0 - 0x1p-40), hi = sc.tol * (1.0 + 0x1p-40);
+        double near_max = 0.0;
+        bool over = false;
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const double y4 = y[i] + h * (c1 * k1[i] + c3 * k3[i] + c4 * k4[i] + c5 * k5[i]);
+            y5[i] = y[i] + h * (d1 * k1[i] + d3 * k3[i] + d4 * k4[i] + d5 * k5[i] + d6 * k6[i]);
+            double scale = fmax(fabs(y[i]), fabs(y5[i]));
+            if (scale < kEps) scale = kEps;
+            const double a = fabs(y5[i] - y4);
+            const double q = a * rcp_nr(scale);
+            over |= q > hi;
+            if (__builtin_expect(q >= lo && q <= hi, 0)) near_max = fmax(near_max, a / scale);
+        }
+        accept = !over && near_max <= sc.tol;
+    } else {
+        double max_error = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const double y4 = y[i] + h * (c1 * k1[i] + c3 * k3[i] + c4 * k4[i] + c5 * k5[i]);
+            y5[i] = y[i] + h * (d1 * k1[i] + d3 * k3[i] + d4 * k4[i] + d5 * k5[i] + d6 * k6[i]);
+            double scale = fmax(fabs(y[i]), fabs(y5[i]));
+            if (scale < kEps) scale = kEps;
+            max_error = fmax(max_error, fabs(y5[i] - y4) / scale);
+        }
+        accept = tol_normal ? max_error <= sc.tol : max_error / sc.tol <= 1.0;
+    }
     if (accept) {
 #pragma unroll
         for (int i = 0; i < 6; i++) y[i] = y5[i];
@@ -1113,15 +1135,16 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 //    shifts, stores). Capped at 128 the allocator spills only inside those blocks -- the hot
 //    blocks are instruction-for-instruction the 3-wave code -- so C2 gains the 4th wave
 //    (+4.6%; C1 neutral).
-//  * BHRT_W_RKF45_KERR (RKF45, a != 0, no disk: C5) = 6 (104 VGPRs = 4 waves by default;
-//    6 waves +4%, 5 +2.6%, 7/8 slower).
+//  * BHRT_W_RKF45_KERR (RKF45, a != 0, no disk: C5) = 5. Before v17: 104 VGPRs = 4 waves
+//    by default, 6 waves +4%, 5 +2.6%, 7/8 slower; with v17's division-free error norm the
+//    6-wave cap spills in the hot blocks and 5 waves is best (+4.2% over v16 at 6).
 //  * C3 (RKF45 a = 0 disk, 200 VGPRs) and C4 (RK4 Kerr disk, 125) keep the compiler's
 //    choice: forcing one more wave spills in their hot blocks (-14%, -1.5%).
 #ifndef BHRT_W_RKF45_DISK
 #define BHRT_W_RKF45_DISK 0
 #endif
 #ifndef BHRT_W_RKF45_KERR
-#define BHRT_W_RKF45_KERR 6
+#define BHRT_W_RKF45_KERR 5
 #endif
 #ifndef BHRT_W_RK4_KERR_DISK
 #define BHRT_W_RK4_KERR_DISK 0
