@@ -20,31 +20,23 @@
 // that many new ray indices from a global queue with ONE atomic and initialises them in
 // the idle lanes (ballot + popcount + lane rank), so a long ray never holds 63 idle lanes.
 //
-// Arithmetic: FP contraction on by default (BHRT_CONTRACT=1; 0 rounds
-// every +,-,* like the reference's x86-64 build); exact divisions without the generic fdiv
-// scaffolding; sincos specialised for the loop's argument range (BHRT_FAST_SINCOS=1, 0 uses
-// OCML), shifted by angle addition between RK stages and carried from one iteration to the
-// next (BHRT_TRIG_CHAIN=1). The hot instantiation contains no call: rays that need a
-// large-argument sincos are re-traced by a second launch (k_trace HUGE=true).
+// Arithmetic: FP contraction on; quotients as a * RN(1/b) without the
+// generic fdiv scaffolding; sincos specialised for the loop's argument range, shifted by angle
+// addition between RK stages and carried from one iteration to the next. The hot
+// instantiation contains no call: rays that need a large-argument sincos are re-traced by a
+// second launch (k_trace HUGE=true).
+//
+// This file holds only the shipped variant. The A/B alternatives measured against it (OCML
+// sincos, exact quotients, unfolded forms, per-iteration trig, the shift-statistics and
+// wave-tail instrumentation) are in git history up to f099035 (tools/build_rev.sh builds any
+// revision for a same-box A/B); DESIGN.md section 6 records what each was worth.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 
 #include "bhrt_kernel.h"
 
-#ifndef BHRT_CONTRACT
-#define BHRT_CONTRACT 1
-#endif
-#ifndef BHRT_FAST_SINCOS
-#define BHRT_FAST_SINCOS 1
-#endif
-#ifndef BHRT_STATS
-#define BHRT_STATS 0
-#endif
-#define BHRT_STATS_N 64
-#if BHRT_CONTRACT
 #pragma clang fp contract(fast)
-#else
-#pragma clang fp contract(off)
-#endif
 
 namespace {
 
@@ -56,99 +48,31 @@ using Scene = bhrt_scene_k;
 struct Counters {
     unsigned rays = 0, iters = 0, full = 0, far_ = 0, kerr = 0;
     bool huge = false;  // a sincos argument needed the large-argument path (see bhrt_sincos)
-#if BHRT_STATS
-    unsigned ds[BHRT_STATS_N] = {};  // instrumented build only (tools/delta_stats.py)
-#endif
 };
 
-#if BHRT_STATS
-// Diagnostic build (make stats): per shift site (0..2 RK stages 2..4, 3..5 the carried
-// advances of y1, y2, y3) lanes and waves whose |delta| exceeds 0.05 / 0.1 / 0.2 / pi/4,
-// plus lane occupancy of the persistent loop. Never part of the product build.
-__device__ unsigned long long g_dstats[BHRT_STATS_N];
-// per wave of the hot k_trace launch: s_memrealtime (100 MHz) at start, when the queue was
-// first seen exhausted, and at exit (tail analysis, tools/wave_tail.py)
-#define BHRT_WAVE_T_MAX 16384
-__device__ unsigned long long g_wave_t[3 * BHRT_WAVE_T_MAX];
-__device__ unsigned g_wave_n;
-// lane-iterations and wave passes per 250 us of a wave's run time (throughput over time)
-#define BHRT_TBINS 128
-__device__ unsigned long long g_tbins[2 * BHRT_TBINS];
-__device__ __forceinline__ void dstat(Counters& n, int site, double delta) {
-    const double thr[4] = {0.05, 0.1, 0.2, 0.78539816339744828};
-    const unsigned long long act = __ballot(1);
-    const bool leader = (threadIdx.x & 63) == __ffsll((long long)act) - 1;
-    unsigned* c = n.ds + site * 10;
-    c[0]++;
-    if (leader) c[1]++;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const bool big = !(fabs(delta) <= thr[j]);
-        if (big) c[2 + j]++;
-        if (__ballot(big) && leader) c[6 + j]++;
-    }
-}
-#endif
-
 // Division without the generic fdiv scaffolding.
-// rcp_nr is the reciprocal refinement the compiler's f64 fdiv performs after v_div_scale
-// (v_rcp_f64 + two Newton steps): RN(1/b) for b in the normal range, and one reciprocal
-// serves every quotient with the same divisor. div_nr(a, b, rcp_nr(b)) is a * RN(1/b)
-// (<= 1.5 ulp; the same order as the FMA contraction of BHRT_CONTRACT): on every BASELINE
-// config it leaves the class and step of every sampled ray equal to the compiled reference's
-// and the hit points as close (profiles/r01_bench_all_configs_v6.jsonl), for 7% of C2.
-// BHRT_EXACT_DIV=1 adds the quotient's residual correction, which makes it bit-identical
-// to a / b (the A/B build "exdiv"). Callers keep the IEEE a / b for out-of-range operands.
-// BHRT_RCP3 (default): one cubically convergent step y0 (1 + e + e^2) instead of two Newton
-// steps -- v_rcp_f64 is good to ~2^-24 (tools/probe/trans_probe.hip), so e^3 ~ 2^-72 is far below
-// the final rounding: the same <= 1 ulp quotient for three FMAs instead of four.
-#ifndef BHRT_RCP3
-#define BHRT_RCP3 1
-#endif
+// rcp_nr is RN(1/b) for b in the normal range: v_rcp_f64 (good to ~2^-24,
+// tools/probe/trans_probe.hip) and one cubically convergent step y0 (1 + e + e^2), e^3 ~ 2^-72
+// far below the final rounding -- three FMAs instead of the compiler's two Newton steps. One
+// reciprocal serves every quotient with the same divisor, and div_nr(a, b, rcp_nr(b)) is
+// a * RN(1/b) (<= 1.5 ulp; the same order as the FMA contraction): on every BASELINE config it
+// leaves the class and step of every sampled ray equal to the compiled reference's and the hit
+// points as close (profiles/r01_bench_all_configs_v6.jsonl), for 7% of C2. Callers keep the
+// IEEE a / b for out-of-range operands.
 __device__ __forceinline__ double rcp_nr(double b) {
-    double y = __builtin_amdgcn_rcp(b);
-    double e = __builtin_fma(-b, y, 1.0);
-#if BHRT_RCP3
+    const double y = __builtin_amdgcn_rcp(b);
+    const double e = __builtin_fma(-b, y, 1.0);
     return __builtin_fma(y, __builtin_fma(e, e, e), y);
-#else
-    y = __builtin_fma(y, e, y);
-    e = __builtin_fma(-b, y, 1.0);
-    return __builtin_fma(y, e, y);
-#endif
 }
-#ifndef BHRT_EXACT_DIV
-#define BHRT_EXACT_DIV 0
-#endif
-__device__ __forceinline__ double div_nr(double a, double b, double yb) {
-    const double q = a * yb;
-#if BHRT_EXACT_DIV
-    return __builtin_fma(__builtin_fma(-b, q, a), yb, q);
-#else
-    (void)b;
-    return q;
-#endif
-}
-// a / 6.0, correctly rounded: RN(1/6) is the exact reciprocal's rounding (Markstein).
-__device__ __forceinline__ __attribute__((unused)) double div6(double a) {
-    constexpr double y = 1.0 / 6.0;
-    const double q = a * y;
-    return __builtin_fma(__builtin_fma(-6.0, q, a), y, q);
-}
+__device__ __forceinline__ double div_nr(double a, double /*b*/, double yb) { return a * yb; }
 
 // fma(a, b, c) with c a compile-time coefficient, as ONE v_fma_f64 whose addend is an SGPR
 // pair (set up by SALU). Left to itself hipcc copies the coefficient into the destination
 // (v_mov_b64) and uses v_fmac_f64: two VALU instructions per Horner step.
-#ifndef BHRT_ASM_FMA
-#define BHRT_ASM_FMA 1
-#endif
 __device__ __forceinline__ double fmac_k(double a, double b, double c) {
-#if BHRT_ASM_FMA
     double r;
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
     return r;
-#else
-    return __builtin_fma(a, b, c);
-#endif
 }
 
 // max(a, b) as ONE v_max_f64 (b in SGPRs): fmax would first canonicalize both operands
@@ -165,12 +89,9 @@ __device__ __forceinline__ double max_raw(double a, double b) {
 // three-constant Cody-Waite reduction with FMA is exact up to a double-double tail. The
 // tail feeds the fdlibm kernels (k_sin.c / k_cos.c, FreeBSD form). Measured on 6e7 random
 // arguments against glibc (the reference's libm): max 1 ulp, 97% bit-identical.
-// |x| >= 2^20, Inf and NaN take OCML's sincos (not inlined: its Payne-Hanek path must not
-// cost registers in the loop).
-#ifndef BHRT_OCML_ATTR
-#define BHRT_OCML_ATTR __attribute__((noinline))
-#endif
-__device__ BHRT_OCML_ATTR void sincos_ocml(double x, double* s, double* c) {
+// |x| >= 2^20 takes OCML's sincos (not inlined: its Payne-Hanek path must not cost registers
+// in the loop).
+__device__ __attribute__((noinline)) void sincos_ocml(double x, double* s, double* c) {
     sincos(x, s, c);
 }
 
@@ -180,12 +101,6 @@ __device__ BHRT_OCML_ATTR void sincos_ocml(double x, double* s, double* c) {
 // Inf and NaN need no special path (the reduction below turns them into NaN, as glibc does).
 __device__ __forceinline__ void bhrt_sincos(double x, double* so, double* co,
                                             Counters* hc = nullptr) {
-#if !BHRT_FAST_SINCOS
-    if (!hc) {
-        sincos(x, so, co);  // OCML
-        return;
-    }
-#endif
     if (!(fabs(x) < 1048576.0)) {
         if (!hc) {
             sincos_ocml(x, so, co);
@@ -228,14 +143,11 @@ __device__ __forceinline__ void bhrt_sincos(double x, double* so, double* co,
     *co = ((q + 1) & 2) ? -cc : cc;
 }
 
-// sin and cos of a + delta from s0 = sin(a), c0 = cos(a). Every
-// RK4/RKF45 stage after the first evaluates ray_derivatives at theta = y1 + delta with a
-// small delta (the stage increment of state[1]; |delta| < 0.09 on a full C2 frame), so one
-// direct sincos per iteration serves all stages: sin(delta) and cos(delta) - 1 come from
-// the fdlibm k_sin / k_cos polynomials and the shift adds only small corrections to s0, c0
-// (error <= the direct value's + 0.5 ulp). Returns false, leaving the outputs unset, when
-// delta is outside [-pi/4, pi/4] or when a + delta - a would not be exact; the caller then
-// evaluates sincos directly.
+// sin and cos of a + delta from s0 = sin(a), c0 = cos(a), delta in
+// [-pi/4, pi/4]: sin(delta) and cos(delta) - 1 from the fdlibm k_sin / k_cos polynomials, and
+// the shift adds only small corrections to s0, c0 (error <= the direct value's + 0.5 ulp).
+// Returns false, leaving the outputs unset, when delta is outside [-pi/4, pi/4] or when
+// a + delta - a would not be exact; the caller then evaluates sincos directly.
 __device__ __forceinline__ bool sincos_shift_wide(double a, double s0, double c0, double x,
                                                   double& s, double& c) {
     const double delta = x - a;  // exact when x in [a/2, 2a] (Sterbenz)
@@ -257,42 +169,17 @@ __device__ __forceinline__ bool sincos_shift_wide(double a, double s0, double c0
     return true;
 }
 
-// sin, cos of x given those of a nearby a, as the trace loop needs them. Nearly every shift is
-// tiny (on a full C2 frame |x - a| > 0.0625 in < 0.7% of wave evaluations at any site,
-// tools/delta_stats.py), so every lane first runs polynomials fitted to |delta| <= 1/16 --
+// sin, cos of x given those of a nearby a, as the trace loop needs them: every RK stage after
+// the first evaluates ray_derivatives at theta = y1 + delta (the stage increment; |delta| < 0.09
+// on a full C2 frame), and the three angles of the state move by one step per iteration.
+// Nearly every shift is tiny (on a full C2 frame |x - a| > 0.0625 in < 0.7% of wave
+// evaluations at any site), so every lane first runs polynomials fitted to |delta| <= 1/16 --
 // three coefficients each for sin(delta) and cos(delta) - 1 instead of fdlibm's six, max error
 // 2.4e-19 / 1.0e-21 (tools/shift_poly_fit.py) -- straight-line, and only a lane outside that
 // interval then redoes the shift with sincos_shift_wide (|delta| <= pi/4) or evaluates directly.
 // The choice is per lane, so a ray's rounding never depends on its wave-mates.
-#ifndef BHRT_SHORT_SHIFT
-#define BHRT_SHORT_SHIFT 1
-#endif
-#ifndef BHRT_SHIFT_FMA2
-#define BHRT_SHIFT_FMA2 1
-#endif
-// The short-interval shift alone (BHRT_SHORT_SHIFT's polynomials); returns true when
-// |x - a| > 1/16, i.e. when the caller must redo s, c with sincos_shift_wide / bhrt_sincos.
-__device__ __forceinline__ __attribute__((unused)) bool short_shift(double a, double s0, double c0, double x, double& s,
-                                            double& c) {
-    const double delta = x - a;
-    constexpr double S1 = -0.16666666666662605, S2 = 0.00833333327878775,
-                     S3 = -0.00019839069723619096;
-    constexpr double C1 = 0.04166666666666157, C2 = -0.0013888888827212717,
-                     C3 = 2.479927034006378e-05;
-    const double z = delta * delta;
-    const double sd = delta + (z * delta) * fmac_k(z, fmac_k(z, S3, S2), S1);
-    const double cm1 = z * __builtin_fma(z, fmac_k(z, fmac_k(z, C3, C2), C1), -0.5);
-    s = __builtin_fma(c0, sd, __builtin_fma(s0, cm1, s0));
-    c = __builtin_fma(-s0, sd, __builtin_fma(c0, cm1, c0));
-    return !(fabs(delta) <= 0.0625);
-}
-#ifndef BHRT_ADV_MERGE
-#define BHRT_ADV_MERGE 0
-#endif
-
 __device__ __forceinline__ void shift_or_eval(double a, double s0, double c0, double x, double& s,
                                               double& c, Counters* hc) {
-#if BHRT_SHORT_SHIFT
     const double delta = x - a;  // exact when |delta| <= |a| / 2 (Sterbenz)
     constexpr double S1 = -0.16666666666662605, S2 = 0.00833333327878775,
                      S3 = -0.00019839069723619096;
@@ -301,66 +188,24 @@ __device__ __forceinline__ void shift_or_eval(double a, double s0, double c0, do
     const double z = delta * delta;
     const double sd = delta + (z * delta) * fmac_k(z, fmac_k(z, S3, S2), S1);  // sin(delta)
     const double cm1 = z * __builtin_fma(z, fmac_k(z, fmac_k(z, C3, C2), C1), -0.5);
-#if BHRT_SHIFT_FMA2
-    // s0 (1 + cm1) + c0 sd as two FMAs (<= 1 ulp instead of ~0.5)
+    // s0 (1 + cm1) + c0 sd as two FMAs (<= 1 ulp)
     s = __builtin_fma(c0, sd, __builtin_fma(s0, cm1, s0));
     c = __builtin_fma(-s0, sd, __builtin_fma(c0, cm1, c0));
-#else
-    s = s0 + (s0 * cm1 + c0 * sd);
-    c = c0 + (c0 * cm1 - s0 * sd);
-#endif
     // (delta = x - a is exact for |x - a| <= |a| / 2 (Sterbenz); otherwise -- a near 0 -- it is
     // off by <= ulp(delta) / 2 <= 3.5e-18, well below the polynomials' rounding)
     if (__builtin_expect(!(fabs(delta) <= 0.0625), 0)) {
         if (!sincos_shift_wide(a, s0, c0, x, s, c)) bhrt_sincos(x, &s, &c, hc);
     }
-#else
-    if (!sincos_shift_wide(a, s0, c0, x, s, c)) bhrt_sincos(x, &s, &c, hc);
-#endif
 }
 
-// ray_derivatives (raytracer.c:44-154). y = (t, r, theta, phi, tdot, rdot) of the caller,
-// read -- as the reference does -- as (r, theta, phi, v_r, v_theta, v_phi).
-// Trig of theta (= y[1]) for one RK stage: stage 1 evaluates it (or, with BHRT_TRIG_CHAIN,
-// takes it from the previous iteration), later stages shift it.
-#ifndef BHRT_TRIG_CHAIN
-#define BHRT_TRIG_CHAIN 1
-#endif
+// Trig of theta (= y[1]) for one RK stage: stage 1 takes it from the previous iteration
+// (carried in Ray_), later stages shift it.
 struct Trig1 {
-    double a = __builtin_nan(""), s = 0.0, c = 0.0;  // theta of stage 1 and its sin, cos;
-#if BHRT_STATS
-    int site = 0;
-#endif
-};                                                   // NaN until stage 1 evaluated them
+    double a, s, c;  // theta of stage 1 and its sin, cos
+};
 
-// HUGE: keep the large-argument sincos path (else flag it, see bhrt_sincos)
-#ifndef BHRT_LAZY_CLAMP
-#define BHRT_LAZY_CLAMP 1
-#endif
-// 1/r and 1/sin(theta) from ONE reciprocal of r sin(theta): one v_rcp_f64 + refinement fewer
-// per stage, <= ~2 ulp instead of 1. Measured -6% at 3 waves/SIMD (v9, longer dependency
-// chain), +1.7% at 4 (v11, profiles/r01_ab_v11_occupancy.txt box 3).
-#ifndef BHRT_ONE_RCP
-#define BHRT_ONE_RCP 1
-#endif
-#ifndef BHRT_REASSOC
-#define BHRT_REASSOC 1
-#endif
-#ifndef BHRT_FOLD_SIXTH
-#define BHRT_FOLD_SIXTH 1
-#endif
-#ifndef BHRT_FOLD_TERM1
-#define BHRT_FOLD_TERM1 1
-#endif
-#ifndef BHRT_TEST_D012
-#define BHRT_TEST_D012 0
-#endif
-#ifndef BHRT_CLAMP_IN_PLAIN
-#define BHRT_CLAMP_IN_PLAIN 1
-#endif
 // ray_derivatives' a = 0 accelerations in the literal form (:92-130, evaluation order as
 // written, divisions as div_nr / IEEE), from sin, cos of the unclamped theta.
-template <bool UNUSED = false>
 __device__ __forceinline__ void accel_literal(const double (&y)[6], double (&d)[6], const Scene& sc,
                                               double st, double ct) {
     double r = y[0];
@@ -382,14 +227,8 @@ __device__ __forceinline__ void accel_literal(const double (&y)[6], double (&d)[
     const double sc4 = st * ct * y[5] * y[5];
     if (r < 1.0e150) {  // r >= 1.5 rs here: every divisor is in the normal range
         const double yr = rcp_nr(r);
-#if BHRT_FOLD_TERM1
-        // -M / (r^2 f) * f == -M / r^2 in exact arithmetic (A/B variant "nofold" keeps it)
+        // -M / (r^2 f) * f == -M / r^2 in exact arithmetic
         const double term1 = -(sc.M * yr) * yr;
-#else
-        const double f = 1.0 - div_nr(sc.rs, r, yr);
-        const double den = rsq * f;
-        const double term1 = -div_nr(sc.M, den, rcp_nr(den)) * f;
-#endif
         d[3] = term1 + term2 + term3;
         d[4] = div_nr(n4, r, yr) + sc4;
         d[5] = div_nr(n5a, r, yr) - div_nr(n5b, st, rcp_nr(st));
@@ -411,7 +250,8 @@ __device__ __forceinline__ void repair_clamp(double (&d)[6]) {
     for (int i = 3; i < 6; i++) d[i] = fmin(fmax(d[i], -10.0), 10.0);
 }
 
-// ray_derivatives (raytracer.c:44-154) for one RK stage; see the block comment above Trig1.
+// ray_derivatives (raytracer.c:44-154) for one RK stage. y = (t, r, theta, phi, tdot, rdot)
+// of the caller, read -- as the reference does -- as (r, theta, phi, v_r, v_theta, v_phi).
 // Stage counters: only FAR instantiations count per stage (a lane's branch varies); otherwise
 // every stage takes the one branch of the instantiation and k_trace derives the count.
 template <bool SPIN0, bool FAR, bool HUGE>
@@ -430,48 +270,27 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
     if (SPIN0) {  // :92-130
         double st, ct;
         if (first) {
-#if BHRT_TRIG_CHAIN
             st = tr.s;  // carried from the previous iteration (ray_iterate)
             ct = tr.c;
-#else
-            bhrt_sincos(y[1], &st, &ct, HUGE ? nullptr : &n);
-            tr.a = y[1];
-            tr.s = st;
-            tr.c = ct;
-#endif
         } else {
-#if BHRT_STATS
-            dstat(n, tr.site++, y[1] - tr.a);
-#endif
             shift_or_eval(tr.a, tr.s, tr.c, y[1], st, ct, HUGE ? nullptr : &n);
         }
         if (FAR) n.full++;
-#if BHRT_REASSOC
-        // Fast form, straight-line: the same three accelerations with the divisions as two
-        // reciprocals and the products regrouped -- d3 = -M/r^2 + r (v_th^2 + (sin th v_ph)^2),
+        // Fast form, straight-line: the same three accelerations with the divisions as one
+        // reciprocal and the products regrouped -- d3 = -M/r^2 + r (v_th^2 + (sin th v_ph)^2),
         // d4 = -2 v_r v_th / r + (sin th v_ph)(cos th v_ph),
         // d5 = -2 v_ph (v_r / r + v_th cos th / sin th) -- a few ulp from the literal
-        // expressions. y[0] is finite (the state is repaired at the top
-        // of every iteration and a stage adds a bounded increment), so fmax is the reference's
-        // clamp. A lane whose result is not a plain |d| <= 10 value (never on a C2 frame)
+        // expressions. y[0] is finite (the state is repaired before
+        // the first iteration or at the top of every iteration, and a stage adds a bounded
+        // increment), so fmax is the reference's clamp. A lane whose result is not a plain
+        // |d| <= 10 value, or whose |sin theta| < 0.01 clamp would bind (never on a C2 frame),
         // recomputes it in the literal form before the repair and clamps.
         const double rc = max_raw(y[0], sc.rs_x1_5);
-#if BHRT_CLAMP_IN_PLAIN
-        // the |sin theta| >= 0.01 clamp of :110-114 never binds on the fast path: a lane where
-        // it would takes the literal form below (never on a C2 frame)
-        const double sc_ = st;
-#else
-        double sc_ = st;
-        if (fabs(st) < 0.01) sc_ = (st >= 0.0) ? 0.01 : -0.01;
-#endif
-#if BHRT_ONE_RCP
-        // 1/r and 1/sin theta from one reciprocal of the product (r sin theta in [0.03, 1e150])
-        const double w = rcp_nr(rc * sc_);
-        const double yr = sc_ * w, ys = rc * w;
-#else
-        const double yr = rcp_nr(rc), ys = rcp_nr(sc_);
-#endif
-        const double u = sc_ * y[5];
+        // 1/r and 1/sin theta from one reciprocal of the product (r sin theta in [0.03, 1e150]):
+        // one v_rcp_f64 + refinement fewer per stage, <= ~2 ulp instead of 1 (+1.7% at 4 waves)
+        const double w = rcp_nr(rc * st);
+        const double yr = st * w, ys = rc * w;
+        const double u = st * y[5];
         const double f3 = rc * __builtin_fma(u, u, y[4] * y[4]);
         d[3] = __builtin_fma(-(sc.M * yr), yr, f3);
         const double p = y[3] * yr;
@@ -482,48 +301,43 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         // derivative is the clamped |d3| <= 10 (or 0), so |state[0]| <= 0.1 * 20 * steps^2;
         // k_path (a caller-given t) and the HUGE redo keep it
         const int plain = (int)(!HUGE ? true : rc < 1.0e150) & (int)(fabs(d[3]) <= 10.0) &
-                          (int)(fabs(d[4]) <= 10.0) & (int)(fabs(d[5]) <= 10.0)
-#if BHRT_CLAMP_IN_PLAIN
-                          & (int)(fabs(st) >= 0.01)
-#endif
-            ;
+                          (int)(fabs(d[4]) <= 10.0) & (int)(fabs(d[5]) <= 10.0) &
+                          (int)(fabs(st) >= 0.01);
         if (__builtin_expect(plain, 1)) return;
         accel_literal(y, d, sc, st, ct);
         repair_clamp(d);
         return;
-#else
-        accel_literal(y, d, sc, st, ct);
-#endif
-    } else {  // :131-138
-        d[3] = 0.0;
-        d[4] = 0.0;
-        d[5] = 0.0;
-        if (FAR) n.kerr++;
     }
-#if BHRT_LAZY_CLAMP
-    // Neither ever applies on a C2 frame (none of 8.3e7 evaluations): one test
-    // per component (NaN and Inf fail |d| <= 10) sends the rare lane through the literal repair.
-    // d[0..2] = y[3..5] need no test: the iteration starts from a finite state (ray_iterate's
-    // loop-top repair), and a stage state's y[3..5] is that state plus h * (coefficients of
-    // |.| <= 8) * k[3..5], which this clamp bounds by 10 -- finite.
-    int plain = (int)(fabs(d[3]) <= 10.0) & (int)(fabs(d[4]) <= 10.0) &
-                (int)(fabs(d[5]) <= 10.0);
-#if BHRT_TEST_D012
-    plain &= (int)isfinite(d[0]) & (int)isfinite(d[1]) & (int)isfinite(d[2]);
-#endif
+    // :131-138
+    d[3] = 0.0;
+    d[4] = 0.0;
+    d[5] = 0.0;
+    if (FAR) n.kerr++;
+    // Far-field and Kerr stages: the repair / clamps never change a value here but run as the
+    // reference's pass whenever a component is not a plain |d| <= 10 value (NaN and Inf fail
+    // the test). d[0..2] = y[3..5] need no test: the iteration starts from a finite state, and
+    // a stage state's y[3..5] is that state plus h * (coefficients of |.| <= 8) * k[3..5],
+    // which the clamp bounds by 10 -- finite.
+    const int plain = (int)(fabs(d[3]) <= 10.0) & (int)(fabs(d[4]) <= 10.0) &
+                      (int)(fabs(d[5]) <= 10.0);
     if (plain) return;
-#endif
     repair_clamp(d);
 }
 
-// (see state_repair below)
-#ifndef BHRT_REPAIR_AT_REFILL
-#define BHRT_REPAIR_AT_REFILL 1
-#endif
+// Where the loop-top state recovery (raytracer.c:543-548) can only ever act on the first
+// iteration, it runs once, at refill (k_trace), and the hot loop drops its 6 VALU per
+// iteration. That holds for RK4 and RKF45 without the far-field branch: every acceleration
+// the loop feeds back is a plain |d| <= 10 value or comes out of the literal repair and clamps
+// (zero on the Kerr branch), so from a finite state a step adds at most h * 10 * (sum of
+// |coefficients| <= 18) to state[3..5] -- a finite double plus that rounds to a finite double
+// -- and h times stage values of state[3..5] (bounded by the initial velocities, |v| < 2^512
+// for any finite set-up, plus 18 per step) to state[0..2], which cannot reach 2^1024 within
+// 2^31 steps. For the same reason RKF45's non-finite-k1 reject (math_util.c:318-333) can
+// never fire there. The far-field branch's 2M / r^2 is unclamped, so far-field instantiations
+// keep both checks every iteration (as does the HUGE redo).
 template <int METHOD, bool FAR, bool HUGE>
 constexpr bool repair_at_refill() {
-    return BHRT_REPAIR_AT_REFILL && (METHOD == INTEGRATOR_RK4 || METHOD == INTEGRATOR_RKF45) &&
-           !FAR && !HUGE;
+    return (METHOD == INTEGRATOR_RK4 || METHOD == INTEGRATOR_RKF45) && !FAR && !HUGE;
 }
 
 // rk4_integrate (math_util.c:162-207) on the six live components; the running sum
@@ -533,9 +347,7 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
                                          Counters& n, Trig1& tr) {
     double k[6], acc[6], yt[6];
     const double hh = 0.5 * h;
-#if BHRT_FOLD_SIXTH
     const double h6 = h * (1.0 / 6.0);
-#endif
     rhs<SPIN0, FAR, HUGE>(y, k, sc, far_ok, n, tr, true);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
@@ -557,13 +369,9 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
     rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
-#if BHRT_FOLD_SIXTH
         // h * (...) / 6 as (h * RN(1/6)) * (...): the increment differs by <= 1 ulp of itself,
-        // which is ~h*|k| / |y| ulp of the state (A/B variant "nosixth" keeps the division)
+        // which is ~h*|k| / |y| ulp of the state
         y[i] = __builtin_fma(h6, acc[i] + k[i], y[i]);
-#else
-        y[i] += div6(h * (acc[i] + k[i]));
-#endif
     }
 }
 
@@ -610,16 +418,18 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
     rhs<SPIN0, FAR, HUGE>(yt, k6, sc, far_ok, n, tr, false);
     double y5[6];
     // :367-391 and :402-434: accept iff RN(max_i RN(|y5_i - y4_i| / scale_i) / tol) <= 1.
-    // For a positive normal tol the outer test is exactly max_error <= tol: x <= t gives
-    // x / t <= 1; x > t means x >= t + ulp(t), so x / t >= 1 + ulp(t) / t > 1 + 2^-53, the
-    // rounding midpoint above 1 (Inf and 0 agree too). That is, every component's RN(a / b)
-    // <= tol. Where the state is provably bounded (repair_at_refill: |b| < 2^600, so 1/b is
-    // normal) a component is decided from q = a * rcp(b), within 2^-50 of a / b: q < tol (1 -
-    // 2^-40) passes, q > tol (1 + 2^-40) rejects, and only a q inside that band (per lane, rare)
-    // takes the IEEE quotient. Other instantiations, and tol <= 0 or subnormal, keep the
-    // literal divisions (wave-uniform branch on tol).
+    // For a positive normal (finite) tol the outer test is exactly max_error <= tol: x <= t
+    // gives x / t <= 1; x > t means x >= t + ulp(t), so x / t >= 1 + ulp(t) / t > 1 + 2^-53, the
+    // rounding midpoint above 1 (x = Inf: Inf / t = Inf > 1, also a reject). That is, every
+    // component's RN(a / b) <= tol. Where the state is provably bounded (repair_at_refill:
+    // |b| < 2^600, so 1/b is normal) a component is decided from q = a * rcp(b), within 2^-50 of
+    // a / b: q < tol (1 - 2^-40) passes, q > tol (1 + 2^-40) rejects, and only a q inside that
+    // band (per lane, rare) takes the IEEE quotient. Other instantiations, and a tol that is
+    // <= 0, subnormal, Inf or NaN, keep the literal final quotient (wave-uniform branch on tol):
+    // tol = Inf with max_error = Inf is Inf / Inf = NaN, a reject, where max_error <= tol would
+    // accept.
     constexpr bool FAST_NORM = repair_at_refill<INTEGRATOR_RKF45, FAR, HUGE>();
-    const bool tol_normal = sc.tol >= 2.2250738585072014e-308;
+    const bool tol_normal = sc.tol >= 2.2250738585072014e-308 && sc.tol <= 1.79769313486231570815e+308;
     bool accept;
     if (FAST_NORM && tol_normal) {
         const double lo = sc.tol * (1.0 - 0x1p-40), hi = sc.tol * (1.0 + 0x1p-40);
@@ -657,17 +467,7 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
     return false;
 }
 
-// spherical_to_cartesian (spacetime.c:229-237)
-__device__ __forceinline__ __attribute__((unused)) void sph2cart(double r, double th, double ph, double& x, double& y,
-                                         double& z, Counters* hc) {
-    double st, ct, sp, cp;
-    bhrt_sincos(th, &st, &ct, hc);
-    bhrt_sincos(ph, &sp, &cp, hc);
-    x = r * st * cp;
-    y = r * st * sp;
-    z = r * ct;
-}
-
+// spherical_to_cartesian (spacetime.c:229-237) from carried sin/cos
 __device__ __forceinline__ void sph2cart_t(double r, double st, double ct, double sp, double cp,
                                            double& x, double& y, double& z) {
     x = r * st * cp;
@@ -675,10 +475,9 @@ __device__ __forceinline__ void sph2cart_t(double r, double st, double ct, doubl
     z = r * ct;
 }
 
-// sin, cos of x from those of a, the same component one iteration earlier:
-// exact shift when sincos_shift's preconditions hold, direct evaluation otherwise. Per ray
-// only (never dependent on which wave runs the ray), so results stay reproducible.
-__device__ __forceinline__ __attribute__((unused)) void trig_advance(double a, double x, double& s, double& c,
+// sin, cos of x from those of a, the same component one iteration earlier.
+// Per ray only (never dependent on which wave runs the ray), so results stay reproducible.
+__device__ __forceinline__ void trig_advance(double a, double x, double& s, double& c,
                                              Counters* hc) {
     double s1, c1;
     shift_or_eval(a, s, c, x, s1, c1, hc);
@@ -716,7 +515,7 @@ struct Ray_ {
     double dx, dy, dz;  // Ray.direction as given (disk test)
     double px, py, pz;  // current Cartesian position; the disk hit point once T_DISK
     double dist;
-    double s1, c1, s2, c2, s3, c3;  // sin, cos of y[1], y[2], y[3] (BHRT_TRIG_CHAIN)
+    double s1, c1, s2, c2, s3, c3;  // sin, cos of y[1], y[2], y[3] (carried)
     int k;              // iterations executed
     bool far_ok;        // use_analytic_approx && impact_parameter > 0
 };
@@ -870,10 +669,8 @@ enum Term : int { T_NONE = 0, T_HORIZON, T_DISK, T_MAXDIST, T_MAXSTEPS };
 struct HSel {  // the four step sizes of the schedule, hoisted out of the kernel argument block
     double far_, r15, r5, r2_5;
 };
-#ifndef BHRT_H_LOCAL
-#define BHRT_H_LOCAL 1
-#endif
-// :543-548, state NaN/Inf recovery at the top of every iteration. One test of the sum
+
+// :543-548, state NaN/Inf recovery at the top of an iteration. One test of the sum
 // (non-finite if any component is, or on overflow); the per-component repair runs only then.
 // ANCHOR = false: the caller knows state[1..3] are finite, so their sin/cos stay valid.
 template <bool ANCHOR = true>
@@ -883,34 +680,22 @@ __device__ __forceinline__ void state_repair(Ray_& R, Counters* hc) {
 #pragma unroll
         for (int i = 0; i < 6; i++)
             if (!isfinite(R.y[i])) R.y[i] = (i < 4) ? 1.0 : 0.0;
-#if BHRT_TRIG_CHAIN
         if (ANCHOR) trig_anchor(R, hc);
-#endif
     }
 }
-// Where the loop-top recovery can only ever act on the first iteration, it runs once, at
-// refill (k_trace), and the hot loop drops its 6 VALU per iteration. That holds for RK4 and
-// RKF45 without the far-field branch: every acceleration the loop feeds back is a plain
-// |d| <= 10 value or comes out of the literal repair and clamps (zero on the Kerr branch), so
-// from a finite state a step adds at most h * 10 * (sum of |coefficients| <= 18) to
-// state[3..5] -- a finite double plus that rounds to a finite double -- and h times stage
-// values of state[3..5] (bounded by the initial velocities, |v| < 2^512 for any finite
-// set-up, plus 18 per step) to state[0..2], which cannot reach 2^1024 within 2^31 steps. For
-// the same reason RKF45's non-finite-k1 reject (math_util.c:318-333) can never fire there.
-// The far-field branch's 2M / r^2 is unclamped, so far-field instantiations keep both checks
-// every iteration (as does the HUGE redo).
 
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
 // on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
+// hs: the step sizes in registers (k_trace), or NULL to read them from the scene.
 template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n,
                                            const HSel* hs = nullptr) {
     Counters* const hc = HUGE ? nullptr : &n;
-    // :543-548. One test of the sum (non-finite if any component is, or on overflow);
-    // the per-component repair runs only then. Instantiations with repair_at_refill() run it
-    // once, when the ray is loaded: there a finite state stays finite (see state_repair).
+    // Instantiations with repair_at_refill() run the recovery once, when the ray is loaded:
+    // there a finite state stays finite.
     if (!repair_at_refill<METHOD, FAR, HUGE>()) state_repair(R, hc);
-    // step schedule (:556-571), written as selects so the first true test wins
+    // step schedule (:556-571), written as selects so the first true test wins; fmin(h, 0.1)
+    // is folded into the values (host)
     const double r = R.y[1];
     double h;
     if (hs) {
@@ -922,17 +707,12 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
         h = sc.h_far;
         h = (r < sc.rs_x15) ? sc.h_15 : h;
         h = (r < sc.rs_x5) ? sc.h_5 : h;
-        h = (r < sc.rs_x2_5) ? sc.h_2_5 : h;  // fmin(h, 0.1) is folded into the values (host)
+        h = (r < sc.rs_x2_5) ? sc.h_2_5 : h;
     }
     bool moved = true;
     if (METHOD != INTEGRATOR_RK4) n.iters++;  // RK4: counted at termination (k_trace)
-    Trig1 tr;
-#if BHRT_TRIG_CHAIN
-    tr.a = R.y[1];
-    tr.s = R.s1;
-    tr.c = R.c1;
+    Trig1 tr{R.y[1], R.s1, R.c1};
     const double a2 = R.y[2], a3 = R.y[3];
-#endif
     if (METHOD == INTEGRATOR_RK4) {
         rk4_step<SPIN0, FAR, HUGE>(R.y, h, sc, R.far_ok, n, tr);
     } else if (METHOD == INTEGRATOR_RKF45) {
@@ -941,39 +721,12 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
         moved = false;  // LEAPFROG / YOSHIDA: "not implemented", state unchanged (:616-624)
     }
     double x, y, z;
-#if BHRT_TRIG_CHAIN
     if (moved) {
-#if BHRT_STATS
-        dstat(n, 3, R.y[1] - tr.a);
-        dstat(n, 4, R.y[2] - a2);
-        dstat(n, 5, R.y[3] - a3);
-#endif
-#if BHRT_ADV_MERGE && BHRT_SHORT_SHIFT
-        // the three advances' short shifts straight-line, then ONE rare-lane branch for any
-        // whose step left |delta| <= 1/16 (same per-lane results as three shift_or_eval calls)
-        double ns1, nc1, ns2, nc2, ns3, nc3;
-        const bool w1 = short_shift(tr.a, R.s1, R.c1, R.y[1], ns1, nc1);
-        const bool w2 = short_shift(a2, R.s2, R.c2, R.y[2], ns2, nc2);
-        const bool w3 = short_shift(a3, R.s3, R.c3, R.y[3], ns3, nc3);
-        if (__builtin_expect(w1 | w2 | w3, 0)) {
-            if (w1 && !sincos_shift_wide(tr.a, R.s1, R.c1, R.y[1], ns1, nc1))
-                bhrt_sincos(R.y[1], &ns1, &nc1, hc);
-            if (w2 && !sincos_shift_wide(a2, R.s2, R.c2, R.y[2], ns2, nc2))
-                bhrt_sincos(R.y[2], &ns2, &nc2, hc);
-            if (w3 && !sincos_shift_wide(a3, R.s3, R.c3, R.y[3], ns3, nc3))
-                bhrt_sincos(R.y[3], &ns3, &nc3, hc);
-        }
-        R.s1 = ns1; R.c1 = nc1; R.s2 = ns2; R.c2 = nc2; R.s3 = ns3; R.c3 = nc3;
-#else
         trig_advance(tr.a, R.y[1], R.s1, R.c1, hc);
         trig_advance(a2, R.y[2], R.s2, R.c2, hc);
         trig_advance(a3, R.y[3], R.s3, R.c3, hc);
-#endif
     }
     sph2cart_t(R.y[1], R.s2, R.c2, R.s3, R.c3, x, y, z);
-#else
-    sph2cart(R.y[1], R.y[2], R.y[3], x, y, z, hc);
-#endif
     const double ox = R.px, oy = R.py, oz = R.pz;
     R.dist += seg_len(x - ox, y - oy, z - oz);
     R.px = x;
@@ -1004,11 +757,8 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
 }
 
 // fill_hit_info (raytracer.c:299-333) / the disk branch of trace_ray (:728-753)
-// sky_tab: the init table's (thetadot, phidot) rows (k_trace with BHRT_SKY_RELOAD, which keeps
-// these two per-ray constants out of registers), or NULL to use R.y6, R.y7.
 __device__ __forceinline__ void store_hit(const bhrt_frame_soa& s, int i, const Ray_& R,
-                                          int term, const Scene& sc,
-                                          const double* sky_tab = nullptr, long n = 0) {
+                                          int term, const Scene& sc) {
     int result, steps;
     double hx, hy, hz, tdil, sx = 0.0, sy = 0.0, sz = 0.0;
     if (term == T_DISK) {
@@ -1026,10 +776,7 @@ __device__ __forceinline__ void store_hit(const bhrt_frame_soa& s, int i, const 
         hy = R.py;
         hz = R.pz;
         tdil = 1.0 / sqrt(1.0 - sc.rs / R.y[1]);
-        if (term == T_MAXDIST) {  // state[5..7]
-            const double y6 = sky_tab ? sky_tab[i] : R.y6, y7 = sky_tab ? sky_tab[n + i] : R.y7;
-            normalize3(R.y[5], y6, y7, sx, sy, sz);
-        }
+        if (term == T_MAXDIST) normalize3(R.y[5], R.y6, R.y7, sx, sy, sz);  // state[5..7]
     }
     if (s.result) s.result[i] = result;
     if (s.steps) s.steps[i] = steps;
@@ -1043,23 +790,13 @@ __device__ __forceinline__ void store_hit(const bhrt_frame_soa& s, int i, const 
     if (s.sky_z) s.sky_z[i] = sz;
 }
 
-#ifndef BHRT_SKY_RELOAD
-#define BHRT_SKY_RELOAD 0
-#endif
-#if BHRT_SKY_RELOAD
-#define SKY_TAB(kp) ((kp).init + 6 * (long)(kp).n)
-#else
-#define SKY_TAB(kp) nullptr
-#endif
 __device__ __forceinline__ void load_init(const bhrt_kparams& kp, int i, Ray_& R) {
     const double* f = kp.init;
     const long n = kp.n;
 #pragma unroll
     for (int j = 0; j < 6; j++) R.y[j] = f[j * n + i];
-#if !BHRT_SKY_RELOAD
     R.y6 = f[6 * n + i];
     R.y7 = f[7 * n + i];
-#endif
     R.dx = f[8 * n + i];
     R.dy = f[9 * n + i];
     R.dz = f[10 * n + i];
@@ -1067,14 +804,12 @@ __device__ __forceinline__ void load_init(const bhrt_kparams& kp, int i, Ray_& R
     R.py = f[12 * n + i];
     R.pz = f[13 * n + i];
     R.far_ok = f[14 * n + i] != 0.0;
-#if BHRT_TRIG_CHAIN
     R.s1 = f[15 * n + i];
     R.c1 = f[16 * n + i];
     R.s2 = f[17 * n + i];
     R.c2 = f[18 * n + i];
     R.s3 = f[19 * n + i];
     R.c3 = f[20 * n + i];
-#endif
     R.dist = 0.0;
     R.k = 0;
 }
@@ -1123,47 +858,27 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
     }
 }
 
-// Persistent trace kernel: grid = what is resident; each wave refills idle lanes from the
-// global queue kp.ctl[0] (one returning atomic per refill, DESIGN.md section 4).
-#ifndef BHRT_WAVES_PER_EU
-#define BHRT_WAVES_PER_EU 0
-#endif
 // Per-instantiation occupancy target (waves per SIMD; 0 = the compiler's choice), same-box
 // A/B in profiles/r01_ab_v11_occupancy.txt:
-//  * BHRT_W_RK4_A0 (RK4, a = 0: C1, C2) = 4. The straight-line iteration needs <= 123 VGPRs;
-//    the register peak (160) sits in the rare-lane blocks (literal accelerations, wide trig
-//    shifts, stores). Capped at 128 the allocator spills only inside those blocks -- the hot
-//    blocks are instruction-for-instruction the 3-wave code -- so C2 gains the 4th wave
-//    (+4.6%; C1 neutral).
-//  * BHRT_W_RKF45_KERR (RKF45, a != 0, no disk: C5) = 5. Before v17: 104 VGPRs = 4 waves
-//    by default, 6 waves +4%, 5 +2.6%, 7/8 slower; with v17's division-free error norm the
-//    6-wave cap spills in the hot blocks and 5 waves is best (+4.2% over v16 at 6).
-//  * C3 (RKF45 a = 0 disk, 200 VGPRs) and C4 (RK4 Kerr disk, 125) keep the compiler's
-//    choice: forcing one more wave spills in their hot blocks (-14%, -1.5%).
-#ifndef BHRT_W_RKF45_DISK
-#define BHRT_W_RKF45_DISK 0
-#endif
-#ifndef BHRT_W_RKF45_KERR
-#define BHRT_W_RKF45_KERR 5
-#endif
-#ifndef BHRT_W_RK4_KERR_DISK
-#define BHRT_W_RK4_KERR_DISK 0
-#endif
-#ifndef BHRT_W_RK4_A0
-#define BHRT_W_RK4_A0 4
-#endif
+//  * RK4, a = 0 (C1, C2): 4. The straight-line iteration needs <= 123 VGPRs; the register
+//    peak (160) sits in the rare-lane blocks (literal accelerations, wide trig shifts,
+//    stores). Capped at 128 the allocator spills only inside those blocks -- the hot blocks
+//    are instruction-for-instruction the 3-wave code -- so C2 gains the 4th wave (+4.6%).
+//  * RKF45, a != 0, no disk (C5): 5. With the division-free error norm the 6-wave cap spills
+//    in the hot blocks and 5 waves is best (+4.2% over 6).
+//  * C3 (RKF45 a = 0 disk) and C4 (RK4 Kerr disk) keep the compiler's choice: forcing one
+//    more wave spills in their hot blocks (-14%, -1.5%).
 template <int METHOD, bool DISK, bool SPIN0>
 constexpr int trace_waves() {
-    return BHRT_WAVES_PER_EU > 0 ? BHRT_WAVES_PER_EU
-         : (METHOD == INTEGRATOR_RKF45 && DISK && SPIN0) ? BHRT_W_RKF45_DISK
-         : (METHOD == INTEGRATOR_RKF45 && !DISK && !SPIN0) ? BHRT_W_RKF45_KERR
-         : (METHOD == INTEGRATOR_RK4 && DISK && !SPIN0) ? BHRT_W_RK4_KERR_DISK
-         : (METHOD == INTEGRATOR_RK4 && SPIN0) ? BHRT_W_RK4_A0
+    return (METHOD == INTEGRATOR_RKF45 && !DISK && !SPIN0) ? 5
+         : (METHOD == INTEGRATOR_RK4 && SPIN0) ? 4
          : 0;
 }
 #define BHRT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, 256), \
                                          amdgpu_waves_per_eu(trace_waves<METHOD, DISK, SPIN0>() > 0 ? trace_waves<METHOD, DISK, SPIN0>() : 1)))
 
+// Persistent trace kernel: grid = what is resident; each wave refills idle lanes from the
+// global queue kp.ctl[0] (one returning atomic per refill, DESIGN.md section 4).
 // FAR: some ray may take ray_derivatives' weak-field branch (origin beyond 15 rs). A camera
 // frame knows this once for all its rays (shared origin); ray arrays always assume it.
 // HUGE = false: the hot instantiation, rays [0, kp.n) from queue head ctl[0]. A ray that
@@ -1193,15 +908,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     int rid = 0;
     bool live = false;
     bool exhausted = false;  // wave-uniform
-#if BHRT_H_LOCAL
     const HSel hsel{kp.sc.h_far, kp.sc.h_15, kp.sc.h_5, kp.sc.h_2_5};
-#endif
-#if BHRT_STATS
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-    unsigned long long t_exh = 0;
-    int tbin = 0;
-    unsigned long long tb_lanes = 0, tb_passes = 0;
-#endif
     for (;;) {
         const unsigned long long live_mask = __ballot(live);
         int n_live = __popcll(live_mask);
@@ -1211,9 +918,6 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             if (lane == 0) base = atomicAdd(head, (unsigned long long)need);
             base = __shfl(base, 0);
             exhausted = base + (unsigned long long)need >= total;
-#if BHRT_STATS
-            if (exhausted) t_exh = __builtin_amdgcn_s_memrealtime();
-#endif
             if (!live) {
                 const unsigned long long id = base + __popcll(~live_mask & below);
                 if (id < total) {
@@ -1237,7 +941,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
-                        store_hit(kp.out, rid, R, T_MAXSTEPS, kp.sc, INL ? nullptr : SKY_TAB(kp), kp.n);
+                        store_hit(kp.out, rid, R, T_MAXSTEPS, kp.sc);
                         live = false;
                     }
                 }
@@ -1248,32 +952,8 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             if (exhausted) break;
             continue;
         }
-#if BHRT_STATS
-        if (lane == 0) {
-            n.ds[60]++;
-            n.ds[61] += n_live;
-            if (exhausted) {  // the tail: passes and live lanes after the queue ran dry
-                n.ds[62]++;
-                n.ds[63] += n_live;
-            }
-            const int b = min((int)((__builtin_amdgcn_s_memrealtime() - t_start) / 25000ull),
-                              BHRT_TBINS - 1);
-            if (b != tbin) {
-                atomicAdd(&g_tbins[2 * tbin], tb_lanes);
-                atomicAdd(&g_tbins[2 * tbin + 1], tb_passes);
-                tbin = b;
-                tb_lanes = tb_passes = 0;
-            }
-            tb_lanes += n_live;
-            tb_passes++;
-        }
-#endif
         if (live) {
-#if BHRT_H_LOCAL
             const int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, &hsel);
-#else
-            const int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n);
-#endif
             if (METHOD == INTEGRATOR_RK4 && (term != T_NONE || (!HUGE && n.huge)))
                 n.iters += R.k;  // every RK4 iteration moves, so R.k = iterations executed
             if (!HUGE && n.huge) {  // hand the ray to the HUGE instantiation
@@ -1282,7 +962,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 kp.redo[atomicAdd(kp.ctl + 6, 1ull)] = rid;
                 live = false;
             } else if (term != T_NONE) {
-                store_hit(kp.out, rid, R, term, kp.sc, INL ? nullptr : SKY_TAB(kp), kp.n);
+                store_hit(kp.out, rid, R, term, kp.sc);
                 live = false;
             }
         }
@@ -1306,23 +986,6 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         if (s3) atomicAdd(kp.ctl + 4, s3);
         if (s4) atomicAdd(kp.ctl + 5, s4);
     }
-#if BHRT_STATS
-    for (int j = 0; j < BHRT_STATS_N; j++) {
-        const unsigned long long v = wave_sum(n.ds[j]);
-        if (lane == 0 && v) atomicAdd(&g_dstats[j], v);
-    }
-    if (!HUGE && lane == 0) {
-        atomicAdd(&g_tbins[2 * tbin], tb_lanes);
-        atomicAdd(&g_tbins[2 * tbin + 1], tb_passes);
-        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-        const unsigned w = atomicAdd(&g_wave_n, 1u);
-        if (w < BHRT_WAVE_T_MAX) {
-            g_wave_t[3 * w] = t_start;
-            g_wave_t[3 * w + 1] = t_exh;
-            g_wave_t[3 * w + 2] = t_end;
-        }
-    }
-#endif
 }
 
 __device__ __forceinline__ double clampd(double v, double lo, double hi) {
@@ -1448,53 +1111,79 @@ __global__ void k_path(const bhrt_kparams kp, double t0, double ox, double oy, d
     store_hit(kp.out, 0, R, term, kp.sc);
 }
 
-int g_cus = 0;
+// ---- launch plumbing --------------------------------------------------------------------
+// Launch geometry is cached per device: a process may drive several devices (bhrt_render_frame
+// splits a frame over every visible one) from several host threads. Every cached value is a
+// pure function of (device, kernel), so concurrent first calls may both compute it and store
+// the same value; the atomics make that race-free without a lock on the launch path.
+constexpr int kMaxDev = 64;
+std::atomic<int> g_cus[kMaxDev];
 
-int grid_for(const void* fn, int n) {
-    if (g_cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (g_cus <= 0) g_cus = 256;
+int current_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
+    return dev;
+}
+
+int device_cus(int dev) {
+    int cus = g_cus[dev].load(std::memory_order_relaxed);
+    if (cus == 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        g_cus[dev].store(cus, std::memory_order_relaxed);
     }
+    return cus;
+}
+
+// resident workgroups of 256 lanes of kernel fn on device dev (the persistent grid)
+int resident_blocks(const void* fn, int dev) {
     int per_cu = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
     if (per_cu <= 0) per_cu = 1;
+    return device_cus(dev) * per_cu;
+}
+
+// grid of a grid-stride elementwise kernel over n items (at most one resident wave of blocks)
+int grid_for(const void* fn, int n) {
     long blocks = ((long)n + 255) / 256;
-    const long cap = (long)g_cus * per_cu;
+    const long cap = resident_blocks(fn, current_device());
     if (blocks > cap) blocks = cap;
     return blocks < 1 ? 1 : (int)blocks;
 }
 
 template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool INL>
 void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
-    static int grid_cap = 0, grid_huge = 0;  // resident workgroups per instantiation
-    if (grid_cap == 0) {
-        grid_cap = grid_for(
-            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, false, INL>), 1 << 30);
-        grid_huge = grid_for(
-            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, true, INL>), 1 << 30);
+    // resident workgroups of the two instantiations, per device
+    static std::atomic<int> grid_cap[kMaxDev], grid_huge[kMaxDev];
+    const int dev = current_device();
+    int cap = grid_cap[dev].load(std::memory_order_relaxed);
+    int cap_huge = grid_huge[dev].load(std::memory_order_relaxed);
+    if (cap == 0 || cap_huge == 0) {
+        cap = resident_blocks(
+            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, false, INL>), dev);
+        cap_huge = resident_blocks(
+            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, true, INL>), dev);
+        grid_cap[dev].store(cap, std::memory_order_relaxed);
+        grid_huge[dev].store(cap_huge, std::memory_order_relaxed);
     }
     int blocks = (kp.n + 255) / 256;
-    if (blocks > grid_cap) blocks = grid_cap;
+    if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, 256, 0, st>>>(kp);
     // rays evicted by the large-argument check (normally none: every wave exits at once)
-    k_trace<METHOD, DISK, SPIN0, FAR, true, INL><<<blocks < grid_huge ? blocks : grid_huge, 256,
-                                                   0, st>>>(kp);
+    k_trace<METHOD, DISK, SPIN0, FAR, true, INL><<<blocks < cap_huge ? blocks : cap_huge, 256, 0,
+                                                   st>>>(kp);
 }
 
-#ifndef BHRT_INLINE_CAMERA
-#define BHRT_INLINE_CAMERA 1
-#endif
 template <int METHOD, bool DISK, bool SPIN0, bool FAR>
 int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     // camera rays set up inside k_trace where rays are short-lived: scenes with a disk (most
     // rays end on it within tens of iterations: C4 +6.6%, C3 +16.5%) except the a = 0 RK4 path
-    // (C2: lifetimes up to max_steps, refills rare; in v10 the set-up code cost that kernel its
-    // third wave per SIMD, and since v11 its hot blocks must fit the 4-wave 128-VGPR cap). Without a disk (C5: rays run ~40 RKF45 attempts to max_distance)
-    // it measured 5% slower (profiles/r01_ab_v10.txt).
-    constexpr bool CAN_INL = BHRT_INLINE_CAMERA && DISK && !(METHOD == INTEGRATOR_RK4 && SPIN0);
+    // (C2: lifetimes up to max_steps, refills rare; its hot blocks must fit the 4-wave 128-VGPR
+    // cap). Without a disk (C5: rays run ~40 RKF45 attempts to max_distance) it measured 5%
+    // slower (profiles/r01_ab_v10.txt).
+    constexpr bool CAN_INL = DISK && !(METHOD == INTEGRATOR_RK4 && SPIN0);
     const bool inl = CAN_INL && kp.src == BHRT_SRC_CAMERA && fabs(kp.cam.r0) < 1048576.0;
     if (inl)
         ;
@@ -1566,50 +1255,6 @@ extern "C" int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0
     default: return dispatch_disk<INTEGRATOR_LEAPFROG>(*kp, st, e0, e1);  // no-op integrators
     }
 }
-
-#if BHRT_STATS
-extern "C" __attribute__((visibility("default"))) int bhrt_debug_stats(unsigned long long* out,
-                                                                      int reset) {
-    int rc = (int)hipDeviceSynchronize();
-    if (!rc) rc = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dstats), sizeof(g_dstats));
-    if (!rc && reset) {
-        static const unsigned long long zero[BHRT_STATS_N] = {};
-        rc = (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dstats), zero, sizeof(zero));
-    }
-    return rc;
-}
-
-// Per-wave (start, queue-exhausted, end) s_memrealtime stamps of the hot k_trace launches
-// since the last reset; returns the number of waves recorded (<= max), or -1.
-extern "C" __attribute__((visibility("default"))) int bhrt_debug_wave_times(
-    unsigned long long* out, int max, int reset) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    unsigned n = 0;
-    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_wave_n), sizeof(n)) != hipSuccess) return -1;
-    if (n > BHRT_WAVE_T_MAX) n = BHRT_WAVE_T_MAX;
-    if ((int)n > max) n = (unsigned)max;
-    if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), 3 * sizeof(unsigned long long) * n) !=
-                 hipSuccess)
-        return -1;
-    if (reset) {
-        const unsigned zero = 0;
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_n), &zero, sizeof(zero)) != hipSuccess) return -1;
-    }
-    return (int)n;
-}
-
-// [2 * BHRT_TBINS] (lane-iterations, wave passes) per 250 us bin of wave run time
-extern "C" __attribute__((visibility("default"))) int bhrt_debug_time_bins(
-    unsigned long long* out, int reset) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tbins), sizeof(g_tbins)) != hipSuccess) return -1;
-    if (reset) {
-        static const unsigned long long zero[2 * BHRT_TBINS] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tbins), zero, sizeof(zero)) != hipSuccess) return -1;
-    }
-    return BHRT_TBINS;
-}
-#endif
 
 extern "C" int bhrt_launch_path(const bhrt_kparams* kp, const double* o4, const double* d3,
                                 Vector3D* d_path, int max_positions, int* d_num, int num_in,
