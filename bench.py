@@ -10,23 +10,30 @@ take the CUs that frame i's tail -- its last, longest rays draining -- leaves id
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--camera B]
 
-N > 1 is launched by torch.distributed.run, one process per GPU.
-  * Weak scaling (C1, C2, C3, C5): every GPU traces the whole configuration frame (1920 x 1080
-    for C2) at its own sub-pixel offset -- rank 0 the pixel centres, rank k the reference's
-    Halton sample k (trace_pixel's jitter) -- so N GPUs supersample the frame with N samples
-    per pixel and every GPU does exactly one frame's work; one RCCL reduce sums the colour
-    planes on rank 0, which divides by N (trace_pixel's sample average, raytracer.c:1096-1164).
-    (A taller image 1080*N rows high is NOT used: with the fixed vertical FOV its horizontal
-    FOV shrinks with N and the per-ray work collapses -- 400 -> 1.6 iterations/ray at N=8.)
-  * Strong scaling (C4): one 3840 x 2160 image split into cyclic 8-row blocks (block b ->
-    rank b % N), un-permuted on rank 0 after the gather.
+N > 1 is launched by torch.distributed.run, one process per GPU. Every frame is an image
+split into cyclic row-block shards (block b -> shard b % S); rank r renders shard r and rank 0
+assembles the colour image of the rendered shards from ONE RCCL gather (configs.Config.frame,
+bhrt/dist_frame.py):
+  * C5 (weak, "weak-shards"): the BASELINE 7680 x 4320 frame in 8 shards of 540 rows (cyclic
+    6-row blocks). N GPUs render shards 0..N-1: N = 1 is shard 0, N = 8 the whole image.
+  * C1-C3 (weak, "weak-tiles"): N x the configuration's pixels at its aspect and field of view
+    (C2: 1920x1080 at N = 1, 2716x1528, 3840x2160, 5433x3056 at N = 2, 4, 8), N shards, so
+    every GPU keeps one configuration frame's worth of rays.
+  * C4 (strong): the one 3840 x 2160 image in N shards.
+  --weak-mode samples (opt-in, C1-C3) instead supersamples the configuration frame: rank k
+  traces it at the reference's Halton sub-pixel offset k and one RCCL reduce averages the
+  colour (trace_pixel's sample average, raytracer.c:1096-1164).
 
 The JSON line also carries:
   roofline      FP64 VALU roofline of the trace kernel: algorithmic FLOPs (SURVEY.md 8(a):
                 117 per RK4 iteration + 35 per a=0 derivative stage + 4 per far-field stage;
-                368 per RKF45 attempt + the same stage costs) / the kernel's GPU time per
-                launch: with overlapping frames the HIP-event busy span of the timed launches
-                (first start to last end) / launches, else the per-launch HIP-event average.
+                368 per RKF45 attempt + the same stage costs; a Kerr stage's accelerations are
+                identically zero, so the 3 velocity components it feeds are not credited:
+                flops()) / the kernel's GPU time per launch: with overlapping frames the
+                HIP-event busy span of the timed launches (first start to last end) /
+                launches, else the per-launch HIP-event average. With a committed PMC
+                summary (profiles/pmc_<config>.json) also the ISSUED FP64 rate: (2 FMA + MUL +
+                ADD + TRANS) f64 wave instructions x 64 lanes per launch / the same duration.
   cpu_baseline  the compiled reference (oracle/_ref/libref.so, unmodified trace_ray under an
                 OpenMP loop) on a row sample of the same frame, rank 0 at N = 1 only; its
                 sampled rows double as the parity check "max |dhit|".
@@ -45,12 +52,15 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from bhrt import abi, configs, lib  # noqa: E402
-from bhrt.dist_frame import FramePipeline, padded_shard_rows, sample_offset  # noqa: E402
+from bhrt.dist_frame import (FramePipeline, padded_shard_rows, sample_offset,  # noqa: E402
+                             shard_row_count)
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (and FP64 matrix) peak, AMD spec
 METRIC = "Mrays/s (and RK4 steps/s) per GPU + per node; max |Δhit| vs CPU ref"
-ROW_BLOCK = 8
 FIELDS = abi.SOA_FIELDS
+# CPU-baseline row sample per config: ~1-3 s wall of the compiled reference on the GPU box's
+# 16 host cores (15-50 core-seconds)
+CPU_ROWS_STRIDE = {"C1": 1, "C2": 27, "C3": 27, "C4": 4, "C5": 3}
 
 
 def parse():
@@ -61,8 +71,9 @@ def parse():
     p.add_argument("--config", default="C2")
     p.add_argument("--camera", default="B")
     p.add_argument("--refill", type=int, default=None)
-    p.add_argument("--cpu-rows-stride", type=int, default=27,
-                   help="CPU baseline samples every k-th image row")
+    p.add_argument("--cpu-rows-stride", type=int, default=None,
+                   help="CPU baseline samples every k-th row of the rendered shard (default "
+                        "per config, ~1-3 s on 16 cores: CPU_ROWS_STRIDE)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true",
                    help="skip the host-buffer leg (its chunked launches would mix into a "
@@ -70,15 +81,34 @@ def parse():
     p.add_argument("--streams", type=int, default=2,
                    help="consecutive frames alternate between this many HIP streams, so the "
                         "next frame's rays fill the CUs the tail of the current frame frees")
+    p.add_argument("--weak-mode", choices=("tiles", "samples"), default="tiles",
+                   help="weak configs at N GPUs: tiles = N shards of a frame (default); "
+                        "samples = N sub-pixel sample planes of the configuration frame "
+                        "(C1-C3), colour averaged by one reduce")
     p.add_argument("--sample", type=int, default=None,
-                   help="weak scaling: trace sample plane K instead of this rank's (to time "
+                   help="samples mode: trace sample plane K instead of this rank's (to time "
                         "each plane of an N-GPU run on one GPU)")
+    p.add_argument("--shard", type=int, default=None,
+                   help="tiles mode, N = 1: render shard K of the frame instead of shard 0 "
+                        "(to time every shard of a node frame on one GPU)")
+    p.add_argument("--gather", choices=("image", "all"), default="image",
+                   help="fields gathered to rank 0: the colour planes (24 B/ray, default) or "
+                        "every SoA field (96 B/ray)")
     return p.parse_args()
 
 
+# SURVEY.md 8(a) op model. An RK4 iteration is 117 ops (96 of them the stage combinations of
+# the 6 live components) + its stages' derivative costs; an RKF45 attempt 368 (347 on the
+# components). A Kerr stage sets d3..d5 = 0 (raytracer.c:131-138), so the combinations of the
+# 3 velocity components it feeds (y + h * sum(b * 0)) are not work: each stage that is NOT a
+# Kerr stage adds its share of those (96 / 2 / 4 = 12 per RK4 stage, 347 / 2 / 6 = 29 per
+# RKF45 stage); the other half stays in the per-iteration base (69 and 194).
 def flops(st, method):
-    per_iter = 368 if method == abi.INTEGRATOR_RKF45 else 117
-    return per_iter * st["iterations"] + 35 * st["stages_full"] + 4 * st["stages_far"]
+    rkf = method == abi.INTEGRATOR_RKF45
+    base, per_live_stage = (194, 29) if rkf else (69, 12)
+    live = st["stages_full"] + st["stages_far"]
+    return (base * st["iterations"] + per_live_stage * live + 35 * st["stages_full"] +
+            4 * st["stages_far"])
 
 
 def main():
@@ -101,19 +131,27 @@ def main():
     c = configs.CONFIGS[args.config]
     bh, dk, cfg = c.scene()
     cam = configs.camera(args.camera)
-    strong = c.scaling == "strong"
-    W, H = c.width, c.bench_height(1)
-    if strong:
-        rows = abi.Rows(ROW_BLOCK, rank, world) if world > 1 else None
-        n = padded_shard_rows(H, ROW_BLOCK, world) * W  # this rank fills its shard_rows
-    else:
-        rows = None
-        n = W * H
+    samples = args.weak_mode == "samples" and c.scaling != "strong"
+    plan = c.frame(1 if samples else world)
+    W, H, S, B = plan.width, plan.height, plan.shards, plan.row_block
+    if samples:
+        if S != 1:
+            raise SystemExit(f"--weak-mode samples needs a one-shard frame ({c.name} is not)")
+        shard, rows, n = 0, None, W * H
         off = sample_offset(rank if args.sample is None else args.sample)
         if off is not None:
             cam.use_offset, cam.offset_x, cam.offset_y = 1, off[0], off[1]
-    pipe = FramePipeline(n, device, world, rank, "shards" if strong else "samples", H, W,
-                         ROW_BLOCK, FIELDS)
+        rays_frame = W * H * world
+    else:
+        shard = rank if args.shard is None or world > 1 else args.shard
+        rows = plan.rows(shard)
+        n = padded_shard_rows(H, B, S) * W  # this rank fills its shard_row_count rows
+        rays_frame = sum(shard_row_count(H, B, r, S) for r in range(world)) * W
+        if args.shard is not None and world == 1:
+            rays_frame = shard_row_count(H, B, shard, S) * W
+    gather = None if args.gather == "all" else dist_frame_rgb()
+    pipe = FramePipeline(n, device, world, rank, "samples" if samples else "shards", H, W, B,
+                         FIELDS, shards=S, gather=gather, first_shard=shard - rank)
     streams = ([torch.cuda.current_stream()] if args.streams <= 1 else
                [torch.cuda.Stream(device) for _ in range(args.streams)])
     frame_no = [0]
@@ -162,7 +200,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    rays_all = float(W * H) * args.steps * (1 if strong else world)
+    rays_all = float(rays_frame) * args.steps
     mrays = rays_all / elapsed / 1e6
     launches = max(st["launches"], 1)
     kern_ms = st["kernel_ms"] / launches
@@ -174,6 +212,17 @@ def main():
     dur_ms = span_ms if len(streams) > 1 else kern_ms
     f_launch = flops(st, c.method) / launches
     achieved = f_launch / (dur_ms * 1e-3) / 1e12
+    prof = pmc_profile(args.config)
+    if samples:
+        parallelism = (f"dp{world}: one sub-pixel sample plane of the frame per GPU ({world} "
+                       "samples/pixel), one RCCL reduce of the colour planes to rank 0 per frame "
+                       "(the sample average, overlapped with the next frame)")
+    else:
+        parallelism = (f"{'single GPU' if world == 1 else f'dp{world}'}: rank r renders shard r "
+                       f"of {S} (cyclic {B}-row blocks)" +
+                       ("" if world == 1 else
+                        f", one RCCL gather of the {args.gather} fields to rank 0 per frame "
+                        "(overlapped with the next frame)"))
     out = {
         "metric": METRIC,
         "value": round(mrays, 3),
@@ -183,25 +232,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": c.scaling,
+        "scaling": "strong" if c.scaling == "strong" else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (deterministic camera-B frame, no input data)",
         "config": {
-            "workload": f"{c.name}: {c.note}",
+            "workload": (f"{c.name}: {c.note}; " +
+                         (f"{W}x{H} frame, sample planes 0..{world - 1}" if samples else
+                          f"{W}x{H} shard {shard}/{S}" if world == 1 and S > 1 else
+                          plan.note)),
             "camera": args.camera,
-            "sample_plane": None if strong else (rank if args.sample is None else args.sample),
+            "sample_plane": (rank if args.sample is None else args.sample) if samples else None,
             "width": W,
             "height": H,
-            "rays_per_gpu": n,
-            "parallelism": ("single GPU" if world == 1 else
-                            (f"dp{world}: cyclic {ROW_BLOCK}-row blocks of one image, one RCCL "
-                             "gather to rank 0 per frame (overlapped with the next frame)")
-                            if strong else
-                            (f"dp{world}: one sub-pixel sample plane of the frame per GPU "
-                             f"({world} samples/pixel), one RCCL reduce of the colour planes "
-                             "to rank 0 per frame (the sample average, overlapped with the "
-                             "next frame)")),
+            "shards": S,
+            "row_block": B,
+            "rays_per_frame": rays_frame,
+            "rays_per_gpu": rays_frame // world if not samples else W * H,
+            "parallelism": parallelism,
         },
         "rk4_steps_per_s": round(iterations_all * (1.0 / elapsed), 1),
         "per_gpu_mrays_s": round(mrays / world, 3),
@@ -222,14 +270,22 @@ def main():
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
-            "traffic": traffic_from_profile(args.config),
+            "flops_per_launch": f_launch,
+            "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
         },
     }
-    if world == 1 and not args.no_host_path:
+    if prof and "issued_fp64_flops_per_launch" in prof:
+        issued = prof["issued_fp64_flops_per_launch"] / (dur_ms * 1e-3) / 1e12
+        out["roofline"].update(
+            issued_fp64_achieved=round(issued, 4),
+            issued_fp64_frac=round(issued / FP64_PEAK_TFLOPS, 5),
+            valu_issue_busy=prof.get("valu_issue_busy"),
+            pmc=f"profiles/pmc_{args.config}.json")
+    if world == 1 and not args.no_host_path and S == 1:  # (bhrt_render_frame: whole images)
         out["host_path"] = host_path_rate(c, bh, dk, cfg, cam, W, H)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["max_rel_dhit"], out["class_mismatch"] = cpu_baseline(
-            args, c, bh, dk, cfg, cam, frame)
+            args, c, bh, dk, cfg, cam, frame, H)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -261,19 +317,25 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=3):
             "note": "bhrt_render_frame into reused host arrays; pipelined chunks"}
 
 
-def traffic_from_profile(config):
-    """HBM bytes per trace-kernel launch from the committed rocprofv3 PMC summary (FETCH_SIZE
-    x2 per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md 'HBM'), or None."""
+def dist_frame_rgb():
+    from bhrt.dist_frame import RGB_FIELDS
+    return RGB_FIELDS
+
+
+def pmc_profile(config):
+    """The committed rocprofv3 PMC summary of the config's trace kernel (tools/pmc_summary.py):
+    HBM bytes per launch (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE,
+    MI355X_MICROARCH.md 'HBM') and issued FP64 work per launch, or None."""
     p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+        return json.load(f)
 
 
-def cpu_baseline(args, c, bh, dk, cfg, cam, frame):
+def cpu_baseline(args, c, bh, dk, cfg, cam, frame, H):
     """The compiled reference (or, if it was not built, the oracle restatement) on every k-th
-    row of the same frame; also the parity of those rows against the GPU frame."""
+    row of rank 0's shard of the same frame; also the parity of those rows against the GPU's."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     try:
@@ -281,9 +343,11 @@ def cpu_baseline(args, c, bh, dk, cfg, cam, frame):
     except (FileNotFoundError, OSError):
         checker, kind = orc.oracle(), "port"
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    W, H = c.width, c.bench_height(1)
-    rows = list(range(0, H, args.cpu_rows_stride))
-    got = {f: frame[f].reshape(H, W).cpu().numpy()[rows] for f in FIELDS}
+    W = frame.local["result"].shape[1]
+    stride = args.cpu_rows_stride or CPU_ROWS_STRIDE.get(c.name, 27)
+    local = list(range(0, len(frame.local_rows), stride))
+    rows = [int(frame.local_rows[j]) for j in local]
+    got = {f: frame.local[f].cpu().numpy()[local] for f in FIELDS}
     t0 = time.perf_counter()
     want = []
     for r in rows:
@@ -302,7 +366,8 @@ def cpu_baseline(args, c, bh, dk, cfg, cam, frame):
                                             np.maximum(np.abs(b[ok]), 1e-9))))
     base = {"value": round(nrays / dt / 1e6, 5), "unit": "Mrays/s", "cores": threads,
             "kind": kind,
-            "sample": f"rows 0,{args.cpu_rows_stride},... of the {W}x{H} frame ({nrays} rays, "
+            "sample": f"every {stride}th row of the {W}x{H} frame's rendered "
+                      f"shard ({nrays} rays, "
                       f"{dt:.1f} s wall, OpenMP over rays; the reference integrates every ray "
                       f"to its full step budget before the disk scan)"}
     return base, worst, mism

@@ -3,6 +3,7 @@
 C1..C5 follow BASELINE.json "configs" in order. Camera B ("inclined 80 deg") is the primary
 camera of every benchmark; A is the README camera, V the visualizer default.
 """
+import math
 from dataclasses import dataclass
 
 from . import abi
@@ -23,6 +24,34 @@ def camera(name="B"):
     return abi.Camera(abi.v3(*c["position"]), abi.v3(*c["direction"]), abi.v3(*c["up"]), c["fov"])
 
 
+def row_block_for(height, shards):
+    """Rows per cyclic block: the largest B <= 8 that splits `height` into `shards` equal
+    shards of whole blocks (C5: 4320 rows / 8 shards -> B = 6, 540 rows each), else 8 (the
+    shards are then padded to whole blocks, dist_frame.padded_shard_rows)."""
+    if shards <= 1:
+        return 8
+    for b in range(8, 0, -1):
+        if height % (b * shards) == 0:
+            return b
+    return 8
+
+
+@dataclass(frozen=True)
+class FramePlan:
+    """What bench.py renders at N GPUs: a width x height image split into
+    `shards` cyclic row-block shards (block b -> shard b % shards, bhrt_rows); rank r renders
+    shard r and rank 0 assembles the image rows of shards 0..N-1 from ONE gather."""
+    width: int
+    height: int
+    shards: int
+    row_block: int
+    note: str
+
+    def rows(self, shard):
+        """bhrt_rows of `shard` (None: the whole image is one shard)."""
+        return abi.Rows(self.row_block, shard, self.shards) if self.shards > 1 else None
+
+
 @dataclass(frozen=True)
 class Config:
     name: str
@@ -36,14 +65,39 @@ class Config:
     flags: int
     gpus: int          # GPUs the configuration is quoted on
     note: str
-    scaling: str = "weak"  # bench.py at N GPUs: "weak" = N x gpu_rows rows, "strong" = height
-    gpu_rows: int = 0      # rows per GPU under weak scaling (0: height)
+    # bench.py at N GPUs (frame()):
+    #   "strong"       the width x height image split into N shards (C4);
+    #   "weak-tiles"   an image with N times the pixels of width x height at the same aspect
+    #                  and field of view, split into N shards: N = 1 is the configuration
+    #                  frame itself and every GPU keeps one frame's worth of rays (C1-C3);
+    #   "weak-shards"  the width x height image is the node frame of `node_shards` GPUs; N
+    #                  GPUs render N of its `node_shards` shards (C5: 7680x4320 in 8 shards of
+    #                  540 rows; N = 1 is shard 0, N = 8 the whole image)
+    scaling: str = "weak-tiles"
+    node_shards: int = 0
 
-    def bench_height(self, n_gpus):
-        """Image rows bench.py renders on n_gpus GPUs."""
-        if self.scaling == "strong":
-            return self.height
-        return (self.gpu_rows or self.height) * n_gpus
+    def frame(self, n_gpus):
+        """The FramePlan of n_gpus GPUs."""
+        n = max(1, int(n_gpus))
+        if self.scaling == "weak-shards":
+            if n > self.node_shards:
+                raise ValueError(f"{self.name}: at most {self.node_shards} GPUs render the "
+                                 f"{self.width}x{self.height} frame's {self.node_shards} shards")
+            S = self.node_shards
+            return FramePlan(self.width, self.height, S, row_block_for(self.height, S),
+                             f"{self.width}x{self.height} frame, shards 0..{n - 1} of {S}")
+        if self.scaling == "strong" or n == 1:
+            return FramePlan(self.width, self.height, n, row_block_for(self.height, n),
+                             f"{self.width}x{self.height} frame in {n} shards")
+        # n x the pixels at the same aspect: height = height * sqrt(n) rounded to a multiple
+        # of n (equal shards; row_block_for picks the block), width from the aspect
+        # (calculate_ray_direction takes aspect = W / H, raytracer.c:1013). n = 4 is exactly
+        # 2x each side (C2: 3840x2160).
+        H = max(n, int(round(self.height * math.sqrt(n) / n)) * n)
+        W = int(round(self.width * H / self.height))
+        return FramePlan(W, H, n, row_block_for(H, n),
+                         f"{W}x{H} frame ({n} x the {self.width}x{self.height} rays at its "
+                         f"aspect and field of view) in {n} shards")
 
     def scene(self):
         bh = abi.black_hole(1.0, self.spin)
@@ -63,6 +117,6 @@ CONFIGS = {
                  abi.BHRT_FLAG_DOPPLER, 8,
                  "3840x2160 Kerr a=0.9 + disk + Doppler/beaming, RK4, 8 GPUs", "strong"),
     "C5": Config("C5", 7680, 4320, 0.99, False, abi.INTEGRATOR_RKF45, 1e-8, 2000, 0, 8,
-                 "7680x4320 Kerr a=0.99, RKF45 tol 1e-8, 2000 steps, 8 GPUs weak scaling: one "
-                 "7680x540 slab per GPU", "weak", 540),
+                 "7680x4320 Kerr a=0.99, RKF45 tol 1e-8, 2000 steps, 8 GPUs weak scaling: "
+                 "shard k/8 (540 rows in cyclic 6-row blocks) per GPU", "weak-shards", 8),
 }

@@ -1,23 +1,30 @@
-"""Multi-GPU frame assembly: one buffer per rank, one gather per frame, pipelined.
+"""Multi-GPU frame assembly: one shard per rank, ONE gather per frame, pipelined.
 
-Each rank renders into ONE contiguous byte buffer holding every SoA field (FrameBuffer), so
-assembling a frame on rank 0 is a single collective (torch.distributed.gather: RCCL on GPUs,
-gloo in the CPU tests). Two ways of splitting the work (FramePipeline.mode):
+A frame is a W x H image split into S cyclic row-block shards (block b -> shard b % S,
+bhrt_rows in include/bhrt_api.h), so the divergent regions (the disk band, the image centre
+against its edges) land on every shard alike. Rank r renders shard r into ONE contiguous byte
+buffer holding every SoA field of its rays (FrameBuffer); the per-ray SoA stays resident on
+its GPU. Rank 0 assembles the image -- by default the colour planes, 24 B per ray -- from a
+single collective (torch.distributed.gather: RCCL over xGMI on GPUs, gloo in the CPU tests):
+the gathered fields are one contiguous byte range of every rank's buffer, so the collective
+reads the render target itself, and rank 0 scatters the N shards into their image rows with
+one strided copy per field. S may exceed the number of ranks (C5: the 7680x4320 frame is 8
+shards of 540 rows; N GPUs render shards 0..N-1 and rank 0 holds those rows of the image).
 
-  * "shards" (strong scaling, one image): cyclic row blocks (block b -> rank b % world;
-    bhrt_rows in include/bhrt_api.h), so the divergent disk band lands on every GPU; rank 0
-    permutes the gathered shards back to image order on the device.
-  * "samples" (weak scaling): every rank traces the whole frame at its own sub-pixel offset
-    (sample_offset: rank 0 the pixel centre, rank k the reference's Halton point k), i.e.
-    the frame is supersampled across GPUs with the per-GPU work of one frame -- trace_pixel's
-    supersampling (raytracer.c:1096-1164) with one sample per GPU. Its exchange is the
-    sample average of the colour: ONE reduce (sum) of the three colour planes to rank 0
-    (24 B per ray instead of the 96 B of a full gather), which divides by the sample count.
-    Every rank's per-ray SoA (hit classes, points, distances) stays resident on its own GPU.
+FramePipeline.mode:
+  * "shards" -- the above (bench.py's default; configs.Config.frame gives W, H, S, B).
+  * "samples" (opt-in) -- every rank traces the whole W x H frame at its own sub-pixel offset
+    (sample_offset: rank 0 the pixel centre, rank k the reference's Halton point k), i.e. the
+    frame is supersampled across GPUs with the per-GPU work of one frame: trace_pixel's
+    supersampling (raytracer.c:1096-1164) with one sample per GPU. The exchange is the sample
+    average of the colour: ONE reduce (sum) of the three colour planes to rank 0, which
+    divides by the sample count.
 
 The collective of frame i runs (on the collective's own stream) while frame i+1 renders; a
 buffer is reused only after the collective that read it has completed (double buffering).
 """
+from dataclasses import dataclass
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -28,41 +35,45 @@ INT_FIELDS = ("result", "steps")
 RGB_FIELDS = ("rgb_r", "rgb_g", "rgb_b")
 
 
-def shard_row_count(H, row_block, shard, world):
-    """Rows owned by `shard` (same rule as bhrt_shard_rows)."""
-    if world <= 1:
+def shard_row_count(H, row_block, shard, num_shards):
+    """Rows owned by `shard` of `num_shards` (same rule as bhrt_shard_rows)."""
+    if num_shards <= 1:
         return H
     n, b = 0, shard
     while b * row_block < H:
         n += min((b + 1) * row_block, H) - b * row_block
-        b += world
+        b += num_shards
     return n
 
 
-def padded_shard_rows(H, row_block, world):
-    """Rows of every shard's buffer in "shards" mode: the largest shard, in whole blocks, so
-    all ranks gather equal-sized buffers. A shard's padding rows map to image rows >= H."""
-    if world <= 1:
+def padded_shard_rows(H, row_block, num_shards):
+    """Rows of every shard's buffer: the largest shard in whole blocks, so all ranks gather
+    equal-sized buffers. A shard's padding rows map to image rows >= H."""
+    if num_shards <= 1:
         return H
-    return -(-H // (row_block * world)) * row_block
+    return -(-H // (row_block * num_shards)) * row_block
 
 
-def shard_rows_index(H, row_block, shard, world):
+def shard_rows_index(H, row_block, shard, num_shards):
     """Image row of each local row of `shard`, in local order."""
-    n = shard_row_count(H, row_block, shard, world)
+    n = shard_row_count(H, row_block, shard, num_shards)
+    if num_shards <= 1:
+        return np.arange(n)
     j = np.arange(n)
-    return ((j // row_block) * world + shard) * row_block + j % row_block
+    return ((j // row_block) * num_shards + shard) * row_block + j % row_block
 
 
 class FrameBuffer:
-    """All SoA fields of n rays carved from one uint8 tensor (8-byte aligned views)."""
+    """All SoA fields of n rays carved from one uint8 tensor (8-byte aligned views): the
+    int32 fields first, then the doubles in the order given (abi.SOA_FIELDS ends with the
+    colour planes, so they form the buffer's contiguous tail)."""
 
     def __init__(self, n, device, fields=abi.SOA_FIELDS):
         self.n = n
         self.fields = tuple(fields)
         sizes = {f: (4 if f in INT_FIELDS else 8) for f in self.fields}
         self.offsets, o = {}, 0
-        for f in sorted(self.fields, key=lambda f: sizes[f]):  # int32 fields first
+        for f in sorted(self.fields, key=lambda f: sizes[f]):  # int32 fields first (stable)
             if sizes[f] == 8:
                 o = (o + 7) // 8 * 8                          # then 8-byte aligned doubles
             self.offsets[f] = (o, o + sizes[f] * n)
@@ -75,29 +86,17 @@ class FrameBuffer:
         a, b = self.offsets[f]
         return buf[a:b].view(torch.int32 if f in INT_FIELDS else torch.float64)
 
+    def span(self, fields):
+        """(first, last) byte of `fields`, which must be one contiguous range of the buffer."""
+        rng = sorted(self.offsets[f] for f in fields)
+        for (_, b), (a, _) in zip(rng, rng[1:]):
+            if a != b:
+                raise ValueError(f"fields {fields} are not contiguous in the frame buffer")
+        return rng[0][0], rng[-1][1]
+
     def soa(self):
         from . import lib
         return lib.soa_from_tensors(self.views)
-
-
-def gather_frame(fb, H, W, row_block, world, rank, gathered=None):
-    """Gather every rank's FrameBuffer to rank 0 and return {field: [H, W] tensor} there
-    (None on other ranks). All shards must hold the same number of rows (pad H to a
-    multiple of world * row_block)."""
-    if world == 1:
-        return {f: fb.views[f].view(H, W) for f in fb.fields}
-    if rank == 0 and gathered is None:
-        gathered = [torch.empty_like(fb.buf) for _ in range(world)]
-    dist.gather(fb.buf, gathered if rank == 0 else None, dst=0)
-    if rank != 0:
-        return None
-    n_rows = fb.n // W
-    img = {}
-    for f in fb.fields:
-        parts = torch.stack([fb.view(g, f) for g in gathered])  # [world, n_rows*W]
-        img[f] = (parts.view(world, n_rows // row_block, row_block, W)
-                  .permute(1, 0, 2, 3).reshape(H, W))
-    return img
 
 
 def sample_offset(k):
@@ -109,35 +108,66 @@ def sample_offset(k):
     return lib.halton(k, 2), lib.halton(k, 3)
 
 
+@dataclass
+class Assembled:
+    """A frame on rank 0.
+    image       {field: [H, W]} of the gathered fields. "shards": the image rows of the
+                rendered shards 0..N-1 (rows of other shards are 0); "samples": the colour
+                averaged over every rank's sample plane.
+    local       {field: [rows, W]} rank 0's own per-ray SoA (every field it rendered).
+    local_rows  image row of each local row."""
+    image: dict
+    local: dict
+    local_rows: np.ndarray
+
+
 class FramePipeline:
     """Double-buffered render -> gather-to-rank-0 -> assemble.
 
-    n = rays per rank buffer: W * H ("samples"), W * padded_shard_rows(...) ("shards", of
-    which a rank renders its first W * shard_row_count(...)).
-    Per frame: fb = next_buffer(); render into fb; submit(). finish() completes the gathers
-    still in flight and returns rank 0's newest assembled frame (None elsewhere):
-      shards:  {field: [H, W]}
-      samples: world > 1 with rgb rendered: {field: [1, H, W]} of rank 0's own sample plane
-               plus "rgb_mean" [3, H, W], the colour averaged over all planes (reduce);
-               without rgb: {field: [world, H, W]}, every plane gathered; world 1: the plane.
+    "shards": rank r renders shard first_shard + r of `shards` (default: world) of the W x H
+    image into
+    next_buffer() (n = W * padded_shard_rows(H, row_block, shards) rays; it fills its first
+    W * shard_row_count(...) of them). "samples": every rank renders the whole W x H frame
+    (n = W * H) at its own sub-pixel offset.
+    `gather`: the fields that travel to rank 0 -- the colour planes by default; they must be
+    a contiguous range of the FrameBuffer (the doubles keep `fields` order).
+    Per frame: fb = next_buffer(); render into fb; submit(). finish() completes the
+    collectives still in flight and returns rank 0's newest Assembled frame (None elsewhere).
     """
 
     def __init__(self, n, device, world, rank, mode, H, W, row_block=8,
-                 fields=abi.SOA_FIELDS):
+                 fields=abi.SOA_FIELDS, shards=None, gather=RGB_FIELDS, first_shard=0):
         assert mode in ("shards", "samples")
         self.world, self.rank, self.mode = world, rank, mode
         self.H, self.W, self.row_block = H, W, row_block
+        self.shards = (shards or world) if mode == "shards" else 1
+        self.first = first_shard  # rank r renders shard first_shard + r
+        if mode == "shards" and not 0 <= first_shard <= self.shards - world:
+            raise ValueError(f"{world} ranks from shard {first_shard} but {self.shards} shards")
         self.bufs = [FrameBuffer(n, device, fields) for _ in range(2)]
-        self.reduce = (mode == "samples" and world > 1 and
-                       all(c in fields for c in RGB_FIELDS))
-        if self.reduce:  # per slot: the colour planes summed over ranks (in place on rank 0)
-            self.colour = [torch.empty(3, n, dtype=torch.float64, device=device)
-                           for _ in range(2)]
-        self.gathered = ([[torch.empty_like(b.buf) for _ in range(world)] for b in self.bufs]
-                         if (world > 1 and rank == 0 and not self.reduce) else None)
+        fb = self.bufs[0]
+        self.gather = tuple(gather) if gather is not None else fb.fields
+        self.span = fb.span(self.gather)
+        if mode == "samples" and world > 1 and not set(self.gather) <= set(RGB_FIELDS):
+            raise ValueError("samples mode reduces the colour planes only")
         self.works = [None, None]
         self.frames = 0
         self.last = None
+        self.images = self.gathered = self.colour = None
+        if mode == "samples":
+            if world > 1:  # per slot: the colour planes summed over ranks (in place on rank 0)
+                self.colour = [torch.empty(len(self.gather), n, dtype=torch.float64,
+                                           device=device) for _ in range(2)]
+            return
+        self.direct = world == 1 and self.shards == 1  # the buffer IS the image
+        if rank == 0 and not self.direct:
+            a, b = self.span
+            # one [world, bytes] receive tensor per slot; gather writes rank k's range to row k
+            self.gathered = [torch.empty(world, b - a, dtype=torch.uint8, device=device)
+                             for _ in range(2)]
+            rows = padded_shard_rows(H, row_block, self.shards) * self.shards
+            self.images = [{f: torch.zeros(rows, W, dtype=fb.views[f].dtype, device=device)
+                            for f in self.gather} for _ in range(2)]
 
     def next_buffer(self):
         slot = self.frames % 2
@@ -146,16 +176,22 @@ class FramePipeline:
 
     def submit(self):
         slot = self.frames % 2
-        if self.reduce:
-            fb, col = self.bufs[slot], self.colour[slot]
-            for i, c in enumerate(RGB_FIELDS):
-                col[i].copy_(fb.views[c])
-            self.works[slot] = dist.reduce(col, dst=0, op=dist.ReduceOp.SUM, async_op=True)
+        fb = self.bufs[slot]
+        a, b = self.span
+        if self.mode == "samples":
+            if self.world > 1:
+                col = self.colour[slot]
+                for i, c in enumerate(self.gather):
+                    col[i].copy_(fb.views[c])
+                self.works[slot] = dist.reduce(col, dst=0, op=dist.ReduceOp.SUM, async_op=True)
+            else:
+                self.works[slot] = True
         elif self.world > 1:
-            self.works[slot] = dist.gather(
-                self.bufs[slot].buf, self.gathered[slot] if self.rank == 0 else None, dst=0,
-                async_op=True)
+            recv = list(self.gathered[slot].unbind(0)) if self.rank == 0 else None
+            self.works[slot] = dist.gather(fb.buf[a:b], recv, dst=0, async_op=True)
         else:
+            if self.gathered is not None:  # one shard of several: place it in the image
+                self.gathered[slot][0].copy_(fb.buf[a:b])
             self.works[slot] = True
         self.frames += 1
 
@@ -174,26 +210,36 @@ class FramePipeline:
         if self.rank == 0:
             self.last = self._assemble(slot)
 
+    def _local(self, fb):
+        if self.mode == "samples":
+            return ({f: fb.views[f].view(self.H, self.W) for f in fb.fields},
+                    np.arange(self.H))
+        idx = shard_rows_index(self.H, self.row_block, self.first, self.shards)
+        rows = fb.n // self.W
+        return {f: fb.views[f].view(rows, self.W)[:len(idx)] for f in fb.fields}, idx
+
     def _assemble(self, slot):
         fb, H, W, world = self.bufs[slot], self.H, self.W, self.world
-        parts = self.gathered[slot] if (world > 1 and not self.reduce) else [fb.buf]
-        img = {}
-        if self.mode == "shards":
+        local, idx = self._local(fb)
+        if self.mode == "samples":
             if world == 1:
-                return {f: fb.views[f].view(H, W) for f in fb.fields}
-            n_rows, B = fb.n // W, self.row_block  # padded_shard_rows
-            for f in fb.fields:
-                p = torch.stack([fb.view(g, f) for g in parts])  # [world, n_rows*W]
-                img[f] = (p.view(world, n_rows // B, B, W).permute(1, 0, 2, 3)
-                          .reshape(world * n_rows, W)[:H])
-            return img
-        if self.reduce:  # rank 0's own plane (sample 0) and the mean colour of all samples
-            img = {f: fb.views[f].view(1, H, W) for f in fb.fields}
-            img["rgb_mean"] = (self.colour[slot] / world).view(3, H, W)
-            return img
-        for f in fb.fields:
-            img[f] = (fb.views[f].view(1, H, W) if world == 1 else
-                      torch.stack([fb.view(g, f) for g in parts]).view(world, H, W))
-        if world > 1 and all(c in img for c in RGB_FIELDS):
-            img["rgb_mean"] = torch.stack([img[c].mean(dim=0) for c in RGB_FIELDS])
-        return img
+                image = {f: local[f] for f in self.gather}
+            else:
+                image = {f: (self.colour[slot][i] / world).view(H, W)
+                         for i, f in enumerate(self.gather)}
+            return Assembled(image, local, idx)
+        if self.direct:
+            return Assembled({f: local[f] for f in self.gather}, local, idx)
+        B, S = self.row_block, self.shards
+        nbk = fb.n // W // B                       # blocks per (padded) shard
+        src_all = self.gathered[slot]
+        a0 = self.span[0]
+        image = {}
+        for f in self.gather:
+            a, b = fb.offsets[f]
+            src = src_all[:, a - a0:b - a0].view(fb.views[f].dtype).view(world, nbk, B, W)
+            dst = self.images[slot][f]
+            dst.view(nbk, S, B, W)[:, self.first:self.first + world].copy_(
+                src.permute(1, 0, 2, 3))
+            image[f] = dst[:H]
+        return Assembled(image, local, idx)

@@ -496,7 +496,72 @@ def spacetime_helpers():
     save("spacetime_helpers", **out)
 
 
+def shader_data():
+    """bh_generate_shader_data (blackhole_api.c:495-608): the 124-byte f32/i32 parameter block
+    the visualizer uploads, for a grid of context states (configured or default disk, spins,
+    simulation settings) and call arguments (show_disk / doppler / redshift flags, sizes, fov,
+    observer vectors). The buffer is pre-filled with a sentinel so untouched words show."""
+    V, I, D, F = C.c_void_p, C.c_int, C.c_double, C.c_float
+    L.bh_initialize.restype = V
+    L.bh_shutdown.argtypes = [V]
+    L.bh_configure_black_hole.argtypes = [V, D, D, D]
+    L.bh_configure_accretion_disk.argtypes = [V, D, D, D, D]
+    L.bh_configure_simulation.argtypes = [V, D, D, I, D]
+    L.bh_generate_shader_data.argtypes = [V, V, V, V, I, I, F, I, I, I, V]
+    L.bh_generate_shader_data.restype = I
+    rng = np.random.default_rng(5)
+    ctx_cases = []  # (mass, spin, disk (inner, outer, T, rho) or None, sim or None)
+    for mass, spin in ((1.0, 0.0), (2.5, 0.5), (1.0, 0.9), (1.0, 0.99), (0.3, 1.0)):
+        for disk in (None, (6.0, 20.0, 1.0, 1.0), (2.3208830417618871, 35.5, 0.7, 2.0)):
+            for sim in (None, (0.05, 250.0, 2000, 1e-8)):
+                ctx_cases.append((mass, spin, disk, sim))
+    ctx_in, call_in, vecs, outs, rcs = [], [], [], [], []
+    for mass, spin, disk, sim in ctx_cases:
+        for k in range(4):
+            ctx = L.bh_initialize()
+            assert L.bh_configure_black_hole(ctx, mass, spin, 0.0) == 0
+            if disk:
+                assert L.bh_configure_accretion_disk(ctx, *disk) == 0
+            if sim:
+                assert L.bh_configure_simulation(ctx, *sim) == 0
+            v = rng.normal(size=(3, 3)).astype(np.float32) * np.float32(20)
+            w, h = int(rng.integers(1, 4000)), int(rng.integers(1, 3000))
+            fov = np.float32(rng.uniform(10.0, 120.0))
+            flags = [int(x) for x in rng.integers(0, 3, size=3)]  # nonzero != 1 included
+            buf = np.full(32, 0x7fbadbad, dtype=np.uint32)
+            rcs.append(L.bh_generate_shader_data(ctx, v[0].ctypes.data, v[1].ctypes.data,
+                                                 v[2].ctypes.data, w, h, F(float(fov)),
+                                                 flags[0], flags[1], flags[2],
+                                                 buf.ctypes.data))
+            L.bh_shutdown(ctx)
+            ctx_in.append([mass, spin] + list(disk or (0, 0, 0, 0)) + list(sim or (0, 0, 0, 0))
+                          + [disk is not None, sim is not None])
+            call_in.append([w, h] + flags)
+            vecs.append(np.concatenate([v.ravel(), [fov]]))
+            outs.append(buf)
+    # argument checks (:508-510): NULL context / vector / buffer
+    ctx = L.bh_initialize()
+    z = np.zeros(3, dtype=np.float32)
+    buf = np.zeros(32, dtype=np.float32)
+    null_rc = [L.bh_generate_shader_data(None, z.ctypes.data, z.ctypes.data, z.ctypes.data, 8, 8,
+                                         F(60.0), 0, 0, 0, buf.ctypes.data),
+               L.bh_generate_shader_data(ctx, None, z.ctypes.data, z.ctypes.data, 8, 8, F(60.0),
+                                         0, 0, 0, buf.ctypes.data),
+               L.bh_generate_shader_data(ctx, z.ctypes.data, z.ctypes.data, z.ctypes.data, 8, 8,
+                                         F(60.0), 0, 0, 0, None)]
+    L.bh_shutdown(ctx)
+    save("shader_data", ctx=np.array(ctx_in, dtype=np.float64),
+         call=np.array(call_in, dtype=np.int64), vecs=np.array(vecs, dtype=np.float32),
+         out=np.array(outs, dtype=np.uint32), rc=np.array(rcs, dtype=np.int64),
+         null_rc=np.array(null_rc, dtype=np.int64))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:]:  # regenerate only the named fixture groups
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
+    shader_data()
     spacetime_helpers()
     particles()
     kat_main()

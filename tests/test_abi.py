@@ -194,3 +194,44 @@ def build_c_demo(tmp_path):
 
 def test_c_demo_links_against_drop_in_headers(tmp_path):
     assert os.path.exists(build_c_demo(tmp_path))
+
+
+def test_shader_data_matches_reference():
+    """bh_generate_shader_data (blackhole_api.c:495-608) writes the reference's 124-byte
+    parameter block bit for bit (tests/golden/shader_data.npz, from the compiled reference)
+    over 120 context / argument combinations, leaves the 32nd word alone, and rejects NULL
+    arguments with the reference's code."""
+    L = lib.load()
+    V, I, D, F = C.c_void_p, C.c_int, C.c_double, C.c_float
+    L.bh_generate_shader_data.argtypes = [V, V, V, V, I, I, F, I, I, I, V]
+    L.bh_generate_shader_data.restype = I
+    g = golden("shader_data")
+    for ctx_in, call, vec, want, rc in zip(g["ctx"], g["call"], g["vecs"], g["out"], g["rc"]):
+        ctx = L.bh_initialize()
+        assert L.bh_configure_black_hole(ctx, ctx_in[0], ctx_in[1], 0.0) == 0
+        if ctx_in[10]:
+            assert L.bh_configure_accretion_disk(ctx, *[float(x) for x in ctx_in[2:6]]) == 0
+        if ctx_in[11]:
+            assert L.bh_configure_simulation(ctx, float(ctx_in[6]), float(ctx_in[7]),
+                                             int(ctx_in[8]), float(ctx_in[9])) == 0
+        v = np.ascontiguousarray(vec[:9].reshape(3, 3), dtype=np.float32)
+        buf = np.full(32, 0x7fbadbad, dtype=np.uint32)
+        got_rc = L.bh_generate_shader_data(ctx, v[0].ctypes.data, v[1].ctypes.data,
+                                           v[2].ctypes.data, int(call[0]), int(call[1]),
+                                           F(float(vec[9])), int(call[2]), int(call[3]),
+                                           int(call[4]), buf.ctypes.data)
+        L.bh_shutdown(ctx)
+        assert got_rc == rc
+        bad = np.nonzero(buf != want)[0]
+        assert bad.size == 0, (ctx_in, call, bad, buf[bad], want[bad])
+    z = np.zeros(3, dtype=np.float32)
+    out = np.zeros(32, dtype=np.float32)
+    ctx = L.bh_initialize()
+    got = [L.bh_generate_shader_data(None, z.ctypes.data, z.ctypes.data, z.ctypes.data, 8, 8,
+                                     F(60.0), 0, 0, 0, out.ctypes.data),
+           L.bh_generate_shader_data(ctx, None, z.ctypes.data, z.ctypes.data, 8, 8, F(60.0), 0,
+                                     0, 0, out.ctypes.data),
+           L.bh_generate_shader_data(ctx, z.ctypes.data, z.ctypes.data, z.ctypes.data, 8, 8,
+                                     F(60.0), 0, 0, 0, None)]
+    L.bh_shutdown(ctx)
+    assert got == list(g["null_rc"])

@@ -216,6 +216,55 @@ def test_full_size_c2_properties(bhrt_lib, oracle):
         assert np.array_equal(frame[f], a[f], equal_nan=True), f
 
 
+def _render_shard(bhrt_lib, c, plan, shard):
+    """bench.py's per-rank render: shard `shard` of the plan's frame through the device API;
+    returns {field: [rows, W] numpy} and the image row of each local row."""
+    import torch
+    from bhrt.dist_frame import shard_rows_index
+    W, H = plan.width, plan.height
+    bh, dk, cfg = c.scene()
+    rows = plan.rows(shard)
+    n = (bhrt_lib.shard_rows(H, rows) if rows else H) * W
+    t = {f: torch.empty(n, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
+                        device="cuda") for f in abi.SOA_FIELDS}
+    bhrt_lib.stats(reset=True)
+    bhrt_lib.render_frame_device(bh, dk, cfg, configs.camera("B"), W, H, rows, c.method,
+                                 c.flags, bhrt_lib.soa_from_tensors(t), None)
+    torch.cuda.synchronize()
+    st = bhrt_lib.stats(reset=True)
+    return ({f: v.cpu().numpy().reshape(-1, W) for f, v in t.items()}, st,
+            shard_rows_index(H, plan.row_block, shard, plan.shards))
+
+
+# BASELINE sizes of the other configs: sampled rows of what bench.py renders at N = 1 (C5:
+# shard 0 of the 7680x4320 frame; C4's whole 3840x2160 image; C3's 1920x1080 frame) and of
+# one more shard of an N-GPU plan, against the oracle rendering the same image rows.
+@pytest.mark.parametrize("cname,n_gpus,shard,stride", [
+    ("C3", 1, 0, 54), ("C4", 1, 0, 135), ("C4", 8, 5, 17), ("C5", 1, 0, 45), ("C5", 8, 7, 45),
+    ("C2", 8, 3, 96)])
+def test_full_size_shard_rows_vs_oracle(bhrt_lib, oracle, cname, n_gpus, shard, stride):
+    c = configs.CONFIGS[cname]
+    plan = c.frame(n_gpus)
+    W, H = plan.width, plan.height
+    got, st, idx = _render_shard(bhrt_lib, c, plan, shard)
+    assert st["rays"] == got["result"].size == len(idx) * W
+    per_stage = 4 if c.method == abi.INTEGRATOR_RK4 else 6
+    assert st["stages_full"] + st["stages_far"] + st["stages_kerr"] == per_stage * st["iterations"]
+    if cname == "C5":  # the 16:9 frame's work per ray (golden frame_C5_B: ~50 attempts)
+        assert 30 < st["iterations"] / st["rays"] < 70, st["iterations"] / st["rays"]
+    local = list(range(0, len(idx), stride))
+    bh, dk, cfg = c.scene()
+    want = {f: [] for f in abi.SOA_FIELDS}
+    for j in local:
+        o = oracle.render_frame(bh, dk, cfg, configs.camera("B"), W, H, c.method, c.flags,
+                                rows=abi.Rows(1, int(idx[j]), H))
+        for f in abi.SOA_FIELDS:
+            want[f].append(o[f])
+    compare({f: got[f][local].ravel() for f in abi.SOA_FIELDS},
+            {f: np.concatenate(v) for f, v in want.items()}, RTOL,
+            c.method != abi.INTEGRATOR_RK4, f"{cname} {W}x{H} shard {shard}/{plan.shards}")
+
+
 def test_device_api_on_torch_stream(bhrt_lib):
     """bhrt_render_frame_device on a torch stream: asynchronous, ordered with torch work."""
     import torch

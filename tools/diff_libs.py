@@ -14,7 +14,7 @@ if sys.argv[1] == "save":
     from bhrt import configs, lib
     c = configs.CONFIGS[sys.argv[2]]
     bh, dk, cfg = c.scene()
-    W, H = c.width, c.bench_height(1)
+    W, H = c.frame(1).width, c.frame(1).height  # (C5: the whole 7680x4320 image)
     f = lib.render_frame(bh, dk, cfg, configs.camera("B"), W, H, c.method, c.flags)
     np.savez(sys.argv[3], **f)
 else:

@@ -13,7 +13,7 @@ i=0
 for grp in "$@"; do
   i=$((i+1))
   echo "== pass $i: $grp"
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex 'k_trace<.*, false>' --output-format csv \
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex 'k_trace<' --output-format csv \
       -d $OUT/p$i -o pass -- python bench.py --config $CFG --steps 1 --warmup 1 --streams 1 --no-cpu-baseline --no-host-path \
       > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done

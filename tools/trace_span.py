@@ -9,20 +9,30 @@ divided by the dispatch count (the GPU busy time per launch, bench.py's roofline
 """
 import argparse
 import csv
+import re
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--kernel", default="k_trace<0, true, true, false, false, false>")
+    ap.add_argument("--kernel", default=None,
+                    help="kernel name (default: the k_trace instantiation with HUGE = false "
+                         "that has the most GPU time in the trace)")
     ap.add_argument("--skip", type=int, default=0, help="leave out the first k dispatches "
                     "(bench.py's untimed warm-up frames)")
     a = ap.parse_args()
-    iv = []
     with open(a.trace) as f:
-        for row in csv.DictReader(f):
-            if a.kernel in row["Kernel_Name"]:
-                iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+        rows = list(csv.DictReader(f))
+    if a.kernel is None:
+        tot = {}
+        for row in rows:
+            k = row["Kernel_Name"]
+            m = re.search(r"k_trace<([^>]*)>", k)
+            if m and m.group(1).split(",")[4].strip() == "false":  # template arg 5 = HUGE
+                tot[k] = tot.get(k, 0) + int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+        a.kernel = max(tot, key=tot.get)
+    iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
+          if a.kernel in r["Kernel_Name"]]
     iv.sort()
     iv = iv[a.skip:]
     n = len(iv)
