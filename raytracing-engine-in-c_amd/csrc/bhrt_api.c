@@ -88,6 +88,7 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 #define BHRT_MAX_DEV 16
 #define BHRT_RING 64        /* control blocks per context             */
 #define BHRT_CTL_WORDS 8    /* u64 per control block (64 B)           */
+#define BHRT_QWORDS ((1 << BHRT_MAX_QUEUE_BITS) * BHRT_QUEUE_STRIDE_MAX) /* queue heads per block */
 #define BHRT_MAX_CHUNKS 8   /* host-buffer frames: pipelined chunks per device            */
 #define BHRT_SCRATCH_SLOTS 4
 #define BHRT_NFIELDS 15
@@ -101,6 +102,7 @@ typedef struct {
     int device;
     hipStream_t stream;
     unsigned long long* d_ctl; /* BHRT_RING x BHRT_CTL_WORDS */
+    unsigned long long* d_q;   /* BHRT_RING x BHRT_QWORDS: ray-queue heads per control block */
     pending_t pend[BHRT_RING];
     int npend, next_slot;
     hipEvent_t evpool[2 * BHRT_RING];
@@ -150,6 +152,37 @@ static int refill_default(const bhrt_scene_k* s) {
     return (s->method == INTEGRATOR_RK4 && s->spin0) ? 8 : 64;
 }
 
+/* Ray queues of k_trace: 2^queue_bits queue heads, queue_stride words apart,
+ * and the claim policy. Every claim is a returning device-scope atomic, and claims on ONE word
+ * serialise at the memory side (~65 M/s): with one queue, C3 (2 M rays of ~2 iterations) ran
+ * at exactly that claim rate. 16 queues: C3 +75%. Where a wave refills only once drained
+ * (refill 64: short-lived rays), a claim also takes a block of ids for the next refills
+ * (claim_div 1: C3 another +25%, C4 +2%); where lanes are refilled as they finish (C2: rays
+ * of 1..1000 iterations) a claim takes exactly the idle lanes -- a block claimed from a stale
+ * estimate of the remainder would hold long rays back into the frame's tail (C2 -17%).
+ * Same-box sweep: profiles/r02_claim_sweep.txt. BHRT_QUEUES (a power of two),
+ * BHRT_QUEUE_STRIDE (words), BHRT_CLAIM_MIN / BHRT_CLAIM_DIV (0 = exactly the idle lanes)
+ * override the defaults. */
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
+static void claim_policy(bhrt_kparams* kp) {
+    int q = env_int("BHRT_QUEUES", 16), bits = 0;
+    while (bits < BHRT_MAX_QUEUE_BITS && (2 << bits) <= q) bits++;
+    int stride = env_int("BHRT_QUEUE_STRIDE", 32);
+    if (stride < 1) stride = 1;
+    if (stride > BHRT_QUEUE_STRIDE_MAX) stride = BHRT_QUEUE_STRIDE_MAX;
+    int m = env_int("BHRT_CLAIM_MIN", 64), d = env_int("BHRT_CLAIM_DIV", kp->refill >= 64);
+    if (m < 64) m = 64;
+    if (m > 1 << 16) m = 1 << 16;
+    kp->queue_bits = bits;
+    kp->queue_stride = stride;
+    kp->claim_min = (m + 63) & ~63;
+    kp->claim_div = d < 0 ? 0 : d;
+}
+
 int bhrt_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -174,6 +207,8 @@ static devctx_t* ctx_get(int device) {
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void**)&c->d_ctl, BHRT_RING * BHRT_CTL_WORDS * sizeof(unsigned long long)) !=
+            hipSuccess ||
+        hipMalloc((void**)&c->d_q, (size_t)BHRT_RING * BHRT_QWORDS * sizeof(unsigned long long)) !=
             hipSuccess) {
         set_err("cannot create HIP stream / control blocks on device %d", device);
         free(c);
@@ -357,6 +392,7 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
         s->disk_out_sq = sqrt_upper_bound(dk->outer_radius);
     }
     kp->refill = g_refill ? g_refill : refill_default(s);
+    claim_policy(kp);
     kp->cam.rows.row_block = 1;
     kp->cam.rows.num_shards = 1;
     return 0;
@@ -427,7 +463,11 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     int slot = c->next_slot;
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
     kp->ctl = c->d_ctl + (size_t)slot * BHRT_CTL_WORDS;
+    kp->qhead = c->d_q + (size_t)slot * BHRT_QWORDS;
     HIP_TRY(hipMemsetAsync(kp->ctl, 0, BHRT_CTL_WORDS * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(kp->qhead, 0,
+                           ((size_t)kp->queue_stride << kp->queue_bits) * sizeof(unsigned long long),
+                           stream));
     if (!c->span_on) {
         HIP_TRY(hipEventRecord(c->span_ref, stream));
         c->span_on = 1;

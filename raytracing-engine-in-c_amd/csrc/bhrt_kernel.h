@@ -20,6 +20,7 @@ extern "C" {
 
 enum { BHRT_SRC_RAYS = 0, BHRT_SRC_CAMERA = 1 };
 enum { BHRT_NUM_COUNTERS = 5 }; /* rays, iterations, stages full/far/kerr */
+enum { BHRT_MAX_QUEUE_BITS = 5, BHRT_QUEUE_STRIDE_MAX = 64 }; /* ray queues of k_trace */
 enum { BHRT_INIT_FIELDS = 21 }; /* y0..y5, y6, y7, dx, dy, dz, px, py, pz, far_ok,
                                    sin/cos of y1, y2, y3 */
 
@@ -60,13 +61,20 @@ typedef struct {
     int src;              /* BHRT_SRC_*                                       */
     int n;                /* rays in this launch                              */
     int refill;           /* refill a wave once >= refill lanes are idle      */
+    int claim_min;        /* smallest block of ray ids a wave claims at once (multiple of 64) */
+    int claim_div;        /* a claim takes (unclaimed rays) / (waves * claim_div), at least
+                             claim_min: large blocks while the queue is full, small at the end */
     const Ray* rays;      /* BHRT_SRC_RAYS: device AoS input                  */
     double* init;         /* [BHRT_INIT_FIELDS][n] initial state (k_init)      */
     int* redo;            /* [n] ids of rays re-traced with the large-argument path */
     bhrt_camera_k cam;    /* BHRT_SRC_CAMERA                                  */
     bhrt_frame_soa out;   /* device SoA outputs; NULL fields skipped          */
-    unsigned long long* ctl; /* [0] queue head, [1..5] counters, [6] redo count,
-                                [7] redo queue head; zeroed per launch */
+    unsigned long long* ctl; /* [1..5] counters, [6] redo count, [7] redo queue head;
+                                zeroed per launch */
+    unsigned long long* qhead; /* ray-queue heads, queue q at qhead[q * queue_stride];
+                                  zeroed per launch */
+    int queue_bits;       /* 2^queue_bits ray queues (<= BHRT_MAX_QUEUE_BITS)            */
+    int queue_stride;     /* u64 words between queue heads (<= BHRT_QUEUE_STRIDE_MAX)     */
 } bhrt_kparams;
 
 /* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and

@@ -874,6 +874,17 @@ constexpr int trace_waves() {
          : (METHOD == INTEGRATOR_RK4 && SPIN0) ? 4
          : 0;
 }
+constexpr int BHRT_TRACE_WAVES_PER_BLOCK = 4;
+
+// Ray queues of k_trace: 64-id block b of the launch belongs to queue b mod 2^qbits; queue q's
+// j-th id and its length.
+__device__ __forceinline__ unsigned queue_ray(unsigned qbits, unsigned q, unsigned j) {
+    return ((j >> 6) << (6u + qbits)) | (q << 6) | (j & 63u);
+}
+__device__ __forceinline__ unsigned queue_size(unsigned ntotal, unsigned qbits, unsigned q) {
+    const unsigned nb = ntotal >> 6, last = nb & ((1u << qbits) - 1u);
+    return (((nb >> qbits) + (q < last ? 1u : 0u)) << 6) + (q == last ? (ntotal & 63u) : 0u);
+}  // k_trace launches 256-lane workgroups
 #define BHRT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, 256), \
                                          amdgpu_waves_per_eu(trace_waves<METHOD, DISK, SPIN0>() > 0 ? trace_waves<METHOD, DISK, SPIN0>() : 1)))
 
@@ -881,7 +892,7 @@ constexpr int trace_waves() {
 // global queue kp.ctl[0] (one returning atomic per refill).
 // FAR: some ray may take ray_derivatives' weak-field branch (origin beyond 15 rs). A camera
 // frame knows this once for all its rays (shared origin); ray arrays always assume it.
-// HUGE = false: the hot instantiation, rays [0, kp.n) from queue head ctl[0]. A ray that
+// HUGE = false: the hot instantiation, rays [0, kp.n) from the queues kp.qhead. A ray that
 // needs a large-argument sincos (bhrt_sincos) is dropped and its id appended to kp.redo
 // (count ctl[6]). HUGE = true: re-traces kp.redo[0, ctl[6]) from queue head ctl[7].
 // INL: camera launch whose rays are set up here, at refill (ray_init_camera), instead of
@@ -890,7 +901,6 @@ constexpr int trace_waves() {
 // The sin/cos anchors of the shared origin are the same for every ray: computed once per wave.
 template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, bool INL = false>
 __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
-    unsigned long long* const head = HUGE ? kp.ctl + 7 : kp.ctl;
     const unsigned long long total =
         HUGE ? *(volatile unsigned long long*)(kp.ctl + 6) : (unsigned long long)kp.n;
     if (total == 0) return;
@@ -907,20 +917,100 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     Ray_ R;
     int rid = 0;
     bool live = false;
-    bool exhausted = false;  // wave-uniform
+    // Ray queues. The rays are dealt, in blocks of 64 consecutive ids, round
+    // robin over Q = 2^queue_bits queues, each with its own head word: every claim is a
+    // returning device-scope atomic, and claims on ONE word serialise at the memory side
+    // (~65 M/s: short-lived scenes -- C3 -- were bound by exactly that rate with one queue).
+    // A wave starts on queue (its index mod Q) and moves on to the next queue when its own
+    // runs dry, never back (a dry queue stays dry). A claim takes the lanes' need; with
+    // claim_div > 0 it takes a block (the queue's unclaimed remainder / (waves * claim_div),
+    // at least claim_min, guided scheduling) that the wave hands out over its next refills.
+    // Per-wave state in LDS (touched only at refill, so it holds no registers across the
+    // loop): [lo, hi) = claimed ids not yet handed out, cur = queue, moves = queues left behind.
+    __shared__ unsigned s_q[BHRT_TRACE_WAVES_PER_BLOCK][4];
+    const unsigned ntotal = (unsigned)total;
+    const unsigned qbits = HUGE ? 0u : (unsigned)kp.queue_bits;
+    const unsigned nq = 1u << qbits;
+    unsigned long long* const heads = HUGE ? kp.ctl + 7 : kp.qhead;
+    const unsigned qstride = HUGE ? 0u : (unsigned)kp.queue_stride;
+    // claim = remainder >> shift, 2^shift >= waves * claim_div / Q (no division in the loop)
+    const unsigned shift =
+        kp.claim_div > 0
+            ? 32u - __builtin_clz((gridDim.x * (blockDim.x >> 6) * kp.claim_div >> qbits) - 1u | 1u)
+            : 0u;
+    const int wv = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_q[wv][0] = 0u;
+        s_q[wv][1] = 0u;
+        s_q[wv][2] = (blockIdx.x * BHRT_TRACE_WAVES_PER_BLOCK + wv) & (nq - 1u);
+        s_q[wv][3] = 0u;
+    }
+    bool exhausted = false;  // every queue dry and the block handed out; wave-uniform
     const HSel hsel{kp.sc.h_far, kp.sc.h_15, kp.sc.h_5, kp.sc.h_2_5};
     for (;;) {
         const unsigned long long live_mask = __ballot(live);
         int n_live = __popcll(live_mask);
         if (!exhausted && (64 - n_live >= kp.refill || n_live == 0)) {
-            const int need = 64 - n_live;
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(head, (unsigned long long)need);
-            base = __shfl(base, 0);
-            exhausted = base + (unsigned long long)need >= total;
+            const unsigned need = 64u - (unsigned)n_live;
+            unsigned lo = __builtin_amdgcn_readfirstlane(s_q[wv][0]);
+            unsigned hi = __builtin_amdgcn_readfirstlane(s_q[wv][1]);
+            unsigned cur = __builtin_amdgcn_readfirstlane(s_q[wv][2]);
+            unsigned moves = __builtin_amdgcn_readfirstlane(s_q[wv][3]);
+            const unsigned avail = hi - lo;
+            const unsigned rank = (unsigned)__popcll(~live_mask & below);
+            unsigned q = cur, j = lo + rank;  // lanes beyond the block take ids of the new claim
+            bool ok = rank < avail;
+            if (avail >= need || moves >= nq) {
+                lo += avail >= need ? need : avail;
+            } else {
+                const unsigned want = need - avail;
+                unsigned b = 0, e = 0;
+                bool hopped = false;
+                for (;;) {  // wave-uniform; at most Q - 1 hops over the wave's life
+                    const unsigned size = queue_size(ntotal, qbits, cur);
+                    unsigned long long* const hp = heads + (size_t)cur * qstride;
+                    unsigned c = want;
+                    if (kp.claim_div > 0 && !hopped) {
+                        c = ((size - hi) >> shift) + 63u & ~63u;
+                        if (c < (unsigned)kp.claim_min) c = (unsigned)kp.claim_min;
+                        if (c < want) c = want;
+                    }
+                    unsigned long long base = 0;
+                    if (lane == 0) {
+                        // a queue reached by a hop may be dry already: look before claiming
+                        if (hopped)
+                            base = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (base < size) base = atomicAdd(hp, (unsigned long long)c);
+                    }
+                    base = __shfl(base, 0);
+                    if (base < size) {
+                        b = (unsigned)base;
+                        e = base + c < size ? (unsigned)(base + c) : size;
+                        break;
+                    }
+                    if (++moves >= nq) break;
+                    cur = (cur + 1u) & (nq - 1u);
+                    hi = 0u;
+                    hopped = true;
+                }
+                if (!ok) {
+                    q = cur;
+                    j = b + (rank - avail);
+                    ok = j < e;
+                }
+                lo = b + want < e ? b + want : e;
+                hi = e;
+            }
+            exhausted = moves >= nq && lo >= hi;
+            if (lane == 0) {
+                s_q[wv][0] = lo;
+                s_q[wv][1] = hi;
+                s_q[wv][2] = cur;
+                s_q[wv][3] = moves;
+            }
             if (!live) {
-                const unsigned long long id = base + __popcll(~live_mask & below);
-                if (id < total) {
+                if (ok) {
+                    const unsigned id = queue_ray(qbits, q, j);
                     rid = HUGE ? kp.redo[id] : (int)id;
                     if (INL) {
                         ray_init_camera(R, kp.cam, rid);
