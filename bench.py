@@ -291,30 +291,67 @@ def main():
         dist.destroy_process_group()
 
 
-def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=3):
+def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
     """bhrt_render_frame into host SoA arrays (allocated and touched once, reused every frame
-    as a render loop does): the PCIe-inclusive rate a C caller of the host API sees. Reported
-    beside `value`, never as it."""
+    as a render loop does): the PCIe-inclusive rate a C caller of the host API sees, one
+    synchronous call per frame, and with bhrt_render_frame_async three frames in flight (three
+    sets of host arrays; frame i+1 traces while frame i is copied). Also the latency of one
+    drop-in trace_ray call. Reported beside `value`, never as it."""
     import ctypes as C
-    arrays, soa = abi.alloc_soa(W * H)
-    for a in arrays.values():
-        a[...] = 0
     L = lib.load()
+    depth = 3  # frames in flight (bhrt_render_frame_async keeps up to 3 per thread)
+    sets = [abi.alloc_soa(W * H) for _ in range(depth)]
+    for arrays, _ in sets:
+        for a in arrays.values():
+            a[...] = 0
+    args = (C.byref(bh), C.byref(dk) if dk else None, C.byref(cfg), C.byref(cam), W, H,
+            c.method, c.flags)
 
-    def frame():
-        if L.bhrt_render_frame(C.byref(bh), C.byref(dk) if dk else None, C.byref(cfg),
-                               C.byref(cam), W, H, c.method, c.flags, C.byref(soa)) != 0:
+    def sync_frame():
+        if L.bhrt_render_frame(*args, C.byref(sets[0][1])) != 0:
             raise RuntimeError(lib.last_error())
 
-    frame()
+    def issue(i):
+        t = C.c_int(0)
+        if L.bhrt_render_frame_async(*args, C.byref(sets[i % depth][1]), C.byref(t)) != 0:
+            raise RuntimeError(lib.last_error())
+        return t.value
+
+    def wait(t):
+        if L.bhrt_frame_wait(t) != 0:
+            raise RuntimeError(lib.last_error())
+
+    sync_frame()
     t0 = time.perf_counter()
     for _ in range(frames):
-        frame()
+        sync_frame()
     dt = (time.perf_counter() - t0) / frames
+    wait(issue(0))
+    t0 = time.perf_counter()
+    pending = [issue(i) for i in range(depth - 1)]
+    for i in range(depth - 1, frames + depth - 1):
+        if i < frames:
+            pending.append(issue(i))
+        wait(pending.pop(0))
+    dta = (time.perf_counter() - t0) / frames
+    # one drop-in trace_ray call (the camera's forward ray), host round trip included
+    ray = abi.Ray(cam.position, cam.direction)
+    hit = abi.RayTraceHit()
+    lat = []
+    for _ in range(12):
+        t = time.perf_counter()
+        L.trace_ray(C.byref(ray), C.byref(bh), C.byref(dk) if dk else None, C.byref(cfg),
+                    C.byref(hit))
+        lat.append(time.perf_counter() - t)
     lib.stats(reset=True)
     return {"mrays_s": round(W * H / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 3),
+            "async_mrays_s": round(W * H / dta / 1e6, 3),
+            "async_ms_per_frame": round(dta * 1e3, 3),
             "bytes_to_host_per_frame": W * H * 96,
-            "note": "bhrt_render_frame into reused host arrays; pipelined chunks"}
+            "trace_ray_latency_ms": round(sorted(lat[2:])[len(lat[2:]) // 2] * 1e3, 3),
+            "note": "bhrt_render_frame into reused host arrays (every field; DMA straight into "
+                    "the page-locked arrays); async = bhrt_render_frame_async with three frames "
+                    "in flight; trace_ray = median of one drop-in call, PCIe round trip included"}
 
 
 def dist_frame_rgb():

@@ -288,6 +288,19 @@ int bhrt_render_frame(const BlackHoleParams* blackhole, const AccretionDiskParam
                       int height, IntegrationMethod method, int flags,
                       const bhrt_frame_soa* host_out);
 
+/* Asynchronous form of bhrt_render_frame: queues the frame and returns a ticket (> 0) in
+ * *ticket; the host arrays receive the frame by DMA while the GPU traces (large frames: the
+ * arrays are page-locked with hipHostRegister for the frame's flight) and must not be read or
+ * freed before bhrt_frame_wait(ticket) returns 0. Three frames may be in flight per host
+ * thread (a fourth waits for the oldest); each needs its own host arrays. */
+int bhrt_render_frame_async(const BlackHoleParams* blackhole, const AccretionDiskParams* disk,
+                            const SimulationConfig* config, const bhrt_camera* camera, int width,
+                            int height, IntegrationMethod method, int flags,
+                            const bhrt_frame_soa* host_out, int* ticket);
+
+/* Wait for a frame queued by bhrt_render_frame_async; 0 when its host arrays are complete. */
+int bhrt_frame_wait(int ticket);
+
 /* Trace n rays already resident on the device (AoS Ray[n]) into DEVICE SoA buffers.
  * method RK4 with disk != NULL is trace_ray; RKF45 with a disk is integrate_photon_path
  * plus trace_ray's disk scan (config C3). */

@@ -39,6 +39,11 @@ _PROTOS = {
     "bhrt_render_frame": (C.c_int, [_P(abi.BlackHoleParams), _P(abi.AccretionDiskParams),
                                     _P(abi.SimulationConfig), _P(abi.Camera), C.c_int, C.c_int,
                                     C.c_int, C.c_int, _P(abi.FrameSoA)]),
+    "bhrt_render_frame_async": (C.c_int, [_P(abi.BlackHoleParams), _P(abi.AccretionDiskParams),
+                                          _P(abi.SimulationConfig), _P(abi.Camera), C.c_int,
+                                          C.c_int, C.c_int, C.c_int, _P(abi.FrameSoA),
+                                          _P(C.c_int)]),
+    "bhrt_frame_wait": (C.c_int, [C.c_int]),
     "bhrt_render_frame_device": (C.c_int, [_P(abi.BlackHoleParams), _P(abi.AccretionDiskParams),
                                            _P(abi.SimulationConfig), _P(abi.Camera), C.c_int,
                                            C.c_int, _P(abi.Rows), C.c_int, C.c_int,

@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #pragma GCC visibility push(default)
 #include "../../include/bhrt_api.h"
@@ -91,6 +92,7 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 #define BHRT_QWORDS ((1 << BHRT_MAX_QUEUE_BITS) * BHRT_QUEUE_STRIDE_MAX) /* queue heads per block */
 #define BHRT_MAX_CHUNKS 8   /* host-buffer frames: pipelined chunks per device            */
 #define BHRT_SCRATCH_SLOTS 4
+#define BHRT_FRAME_SLOTS 3  /* host-buffer frames in flight per thread (bhrt_render_frame_async) */
 #define BHRT_NFIELDS 15
 
 typedef struct {
@@ -127,6 +129,15 @@ typedef struct {
      * copy stream, and per chunk: trace finished / its D2H landed */
     hipStream_t stream2, copy;
     hipEvent_t chunk_done[BHRT_MAX_CHUNKS], chunk_copied[BHRT_MAX_CHUNKS];
+    /* per frame slot of bhrt_render_frame_async: device SoA of every chunk, pinned staging
+     * (only when the caller's arrays cannot be registered), chunk traced / chunk copied */
+    struct {
+        void* d_soa;
+        size_t cap_soa;
+        void* h_stage;
+        size_t cap_stage;
+        hipEvent_t done[BHRT_MAX_CHUNKS], copied[BHRT_MAX_CHUNKS];
+    } fr[BHRT_FRAME_SLOTS];
     /* busy span of the trace kernels since the last stats reset: span_ref is recorded before
      * the first launch; [span_lo, span_hi] = earliest start / latest end relative to it (ms).
      * With launches overlapping on several streams, span / launches is the GPU time per
@@ -238,6 +249,14 @@ static devctx_t* ctx_get(int device) {
             free(c);
             return NULL;
         }
+    for (int f = 0; f < BHRT_FRAME_SLOTS; f++)
+        for (int i = 0; i < BHRT_MAX_CHUNKS; i++)
+            if (hipEventCreateWithFlags(&c->fr[f].done[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->fr[f].copied[i], hipEventDisableTiming) != hipSuccess) {
+                set_err("hipEventCreate failed");
+                free(c);
+                return NULL;
+            }
     g_ctx[device] = c;
     return c;
 }
@@ -710,14 +729,167 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
     return 0;
 }
 
-/* Host-buffer frames are traced in K chunks per device -- cyclic row-block shards k*ndev + d
- * of K*ndev, so every chunk carries the same mix of work -- alternating between two trace
- * streams, so a chunk's workgroups fill the CUs its predecessor's tail (the longest rays)
- * frees. A copy stream moves each finished chunk into pinned staging while later ones trace,
- * and the host un-permutes a chunk into the caller's arrays as soon as it lands. */
-int bhrt_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* dk,
-                      const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
-                      IntegrationMethod method, int flags, const bhrt_frame_soa* host) {
+/* ---- host-buffer frames (bhrt_render_frame[_async]) ---- */
+/* A frame is traced in K chunks per device -- cyclic row-block shards k*ndev + d of K*ndev, so
+ * every chunk carries the same mix of work -- alternating between two trace streams, so a
+ * chunk's workgroups fill the CUs its predecessor's tail (the longest rays) frees. While the
+ * GPU traces, the host registers the caller's arrays (hipHostRegister: ~1.7 ms for a C2 frame's
+ * 199 MB of touched pages), and each finished chunk is copied by DMA straight into them on the
+ * copy stream: one 2-D copy per field un-permutes the row blocks, so no byte passes through
+ * the CPU. Arrays that cannot be registered take pinned staging and a host un-permute at
+ * wait time. DESIGN.md §4 "Host-buffer frames". */
+typedef struct {
+    int active, ticket, ndev, K, shards, W, H, direct, nreg;
+    int timing;             /* BHRT_HOST_TIMING: print where the frame's time went (device 0) */
+    hipEvent_t t_ev[2 + 2 * BHRT_MAX_CHUNKS];
+    double t_host[4];
+    bhrt_frame_soa host;
+    shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
+    bhrt_rows rows[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
+    size_t stage_off[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
+    void* reg[BHRT_NFIELDS]; /* page ranges this frame registered (unregistered at wait) */
+} host_frame;
+
+static _Thread_local host_frame* g_frames; /* [BHRT_FRAME_SLOTS], allocated on first use */
+static _Thread_local int g_next_ticket;
+
+static void unregister_host(host_frame* f) {
+    for (int i = 0; i < f->nreg; i++) (void)hipHostUnregister(f->reg[i]);
+    f->nreg = 0;
+}
+
+/* Register the pages of every field the caller asked for (merged into disjoint ranges). Pages
+ * the caller registered itself are used as they are. Returns 0 when every field is DMA-able. */
+static int register_host(host_frame* f) {
+    const uintptr_t pg = 4096;
+    uintptr_t a[BHRT_NFIELDS], b[BHRT_NFIELDS];
+    int n = 0;
+    for (int k = 0; k < BHRT_NFIELDS; k++) {
+        const uintptr_t p = (uintptr_t)*soa_slot(&f->host, k);
+        if (!p) continue;
+        const uintptr_t lo = p & ~(pg - 1),
+                        hi = (p + k_fsize[k] * (size_t)f->W * (size_t)f->H + pg - 1) & ~(pg - 1);
+        int i = n++; /* insertion sort by start */
+        while (i > 0 && a[i - 1] > lo) {
+            a[i] = a[i - 1];
+            b[i] = b[i - 1];
+            i--;
+        }
+        a[i] = lo;
+        b[i] = hi;
+    }
+    f->nreg = 0;
+    for (int i = 0; i < n;) {
+        uintptr_t lo = a[i], hi = b[i];
+        for (i++; i < n && a[i] <= hi; i++)
+            if (b[i] > hi) hi = b[i];
+        const hipError_t e = hipHostRegister((void*)lo, hi - lo, hipHostRegisterPortable);
+        if (e == hipSuccess) {
+            f->reg[f->nreg++] = (void*)lo;
+        } else {
+            (void)hipGetLastError();
+            if (e != hipErrorHostMemoryAlreadyRegistered) {
+                unregister_host(f);
+                return -1;
+            }
+        }
+    }
+    return 0;
+}
+
+/* DMA a finished chunk's wanted fields straight into the (registered) caller arrays: local
+ * row block i of shard sh is image block i*S + sh, so the full blocks are one 2-D copy per
+ * field and a partial last block one more copy. */
+static int copy_chunk_direct(const shard_job* j, const bhrt_frame_soa* host, int W,
+                             const bhrt_rows* rows, hipStream_t st) {
+    for (int f = 0; f < BHRT_NFIELDS; f++) {
+        if (!WANTED(j, host, f)) continue;
+        char* dst = (char*)*soa_slot((bhrt_frame_soa*)host, f);
+        const char* src = (const char*)*soa_slot((bhrt_frame_soa*)&j->dev, f);
+        const size_t fs = k_fsize[f];
+        if (!rows || rows->num_shards <= 1) {
+            HIP_TRY(hipMemcpyAsync(dst, src, fs * (size_t)j->n, hipMemcpyDeviceToHost, st));
+            continue;
+        }
+        const size_t rowb = fs * (size_t)W, B = rows->row_block, S = rows->num_shards,
+                     sh = rows->shard;
+        const size_t nrow = (size_t)j->n / W, nfull = nrow / B, rem = nrow % B;
+        if (nfull)
+            HIP_TRY(hipMemcpy2DAsync(dst + sh * B * rowb, S * B * rowb, src, B * rowb, B * rowb,
+                                     nfull, hipMemcpyDeviceToHost, st));
+        if (rem)
+            HIP_TRY(hipMemcpyAsync(dst + (nfull * S + sh) * B * rowb, src + nfull * B * rowb,
+                                   rem * rowb, hipMemcpyDeviceToHost, st));
+    }
+    return 0;
+}
+
+/* Chunks per device: each chunk's copy overlaps the tracing of the next, so only the last
+ * chunk's copy follows the trace; but a chunk of C2 is traced by a full-chip persistent grid,
+ * and below ~2 rays per resident lane a chunk is all tail. C2 (2 M rays), same box, ms per
+ * frame for 1/2/3/4/8 chunks: synchronous 16.9/17.0/14.4/11.5-11.9/19.1, three frames in
+ * flight 1 chunk 12.2-12.6, 4 chunks 10.3-10.4 (profiles/r02_host_path.txt). */
+static int frame_chunks(int ndev, int W, int H, int block) {
+    const long per_dev = (long)W * H / ndev;
+    int K = per_dev >= (1L << 20) ? 4 : (per_dev >= (1L << 18) ? 2 : 1);
+    const char* env = getenv("BHRT_HOST_CHUNKS");
+    if (env && atoi(env) >= 1 && atoi(env) <= BHRT_MAX_CHUNKS) K = atoi(env);
+    while (K > 1 && H < K * ndev * block) K--;
+    return K;
+}
+
+int bhrt_frame_wait(int ticket) {
+    if (!g_frames || ticket <= 0) {
+        set_err("no such frame ticket %d", ticket);
+        return -1;
+    }
+    host_frame* f = &g_frames[ticket % BHRT_FRAME_SLOTS];
+    if (!f->active || f->ticket != ticket) {
+        set_err("frame ticket %d is not in flight", ticket);
+        return -1;
+    }
+    f->active = 0;
+    int rc = 0;
+    struct timespec tw0;
+    clock_gettime(CLOCK_MONOTONIC, &tw0);
+    for (int k = 0; k < f->K && rc == 0; k++)
+        for (int d = 0; d < f->ndev && rc == 0; d++) {
+            devctx_t* c = f->jobs[k][d].c;
+            const int slot = ticket % BHRT_FRAME_SLOTS;
+            if (hipSetDevice(d) != hipSuccess || hipEventSynchronize(c->fr[slot].copied[k]) != hipSuccess) {
+                set_err("frame %d: waiting for chunk %d of device %d failed", ticket, k, d);
+                rc = -1;
+                break;
+            }
+            if (!f->direct)
+                readback_finish(&f->jobs[k][d], &f->host,
+                                (const char*)c->fr[slot].h_stage + f->stage_off[k][d], f->W,
+                                f->shards > 1 ? &f->rows[k][d] : NULL);
+        }
+    unregister_host(f);
+    if (f->timing && rc == 0) {
+        struct timespec tw1;
+        clock_gettime(CLOCK_MONOTONIC, &tw1);
+        float tr[BHRT_MAX_CHUNKS], cp[BHRT_MAX_CHUNKS];
+        for (int k = 0; k < f->K; k++) {
+            (void)hipEventElapsedTime(&tr[k], f->t_ev[0], f->t_ev[2 + 2 * k]);
+            (void)hipEventElapsedTime(&cp[k], f->t_ev[0], f->t_ev[3 + 2 * k]);
+        }
+        fprintf(stderr, "libbhrt frame %d (%s, K=%d): enqueue %.2f ms, register %.2f ms, copies "
+                "queued %.2f ms, wait %.2f ms |", ticket, f->direct ? "direct" : "staging", f->K,
+                f->t_host[0], f->t_host[1], f->t_host[2],
+                (tw1.tv_sec - tw0.tv_sec) * 1e3 + (tw1.tv_nsec - tw0.tv_nsec) * 1e-6);
+        for (int k = 0; k < f->K; k++) fprintf(stderr, " chunk %d traced %.2f copied %.2f", k, tr[k], cp[k]);
+        fprintf(stderr, "\n");
+    }
+    return rc;
+}
+
+static int render_frame_issue(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                              const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                              IntegrationMethod method, int flags, const bhrt_frame_soa* host,
+                              int* ticket_out) {
+    if (ticket_out) *ticket_out = 0;
     if (check_scene(bh, cfg) || !cam || !host || W <= 0 || H <= 0) {
         if (!g_err[0]) set_err("invalid argument");
         return -1;
@@ -727,66 +899,127 @@ int bhrt_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* dk,
         set_err("no HIP device available (libbhrt has no CPU path)");
         return -1;
     }
+    if (!g_frames && !(g_frames = (host_frame*)calloc(BHRT_FRAME_SLOTS, sizeof(host_frame)))) {
+        set_err("host allocation failed");
+        return -1;
+    }
+    const int ticket = ++g_next_ticket, slot = ticket % BHRT_FRAME_SLOTS;
+    host_frame* f = &g_frames[slot];
+    if (f->active && bhrt_frame_wait(f->ticket)) return -1; /* the slot's previous frame */
     const int block = 8;
     if (ndev > 1 && H < ndev * block) ndev = 1;
-    const long per_dev = (long)W * H / ndev;  /* chunks per device: */
-    int K = per_dev >= (1L << 20) ? 8 : (per_dev >= (1L << 18) ? 4 : 1);
-    if (H < K * ndev * block) K = 1;
-    const char* env = getenv("BHRT_HOST_CHUNKS");
-    if (env && atoi(env) >= 1 && atoi(env) <= BHRT_MAX_CHUNKS && H >= atoi(env) * ndev * block)
-        K = atoi(env);
-    const int shards = K * ndev;
-    shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
-    bhrt_rows rows[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
-    size_t stage_off[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
+    const int K = frame_chunks(ndev, W, H, block), shards = K * ndev;
+    f->ticket = ticket;
+    f->ndev = ndev;
+    f->K = K;
+    f->shards = shards;
+    f->W = W;
+    f->H = H;
+    f->host = *host;
+    f->nreg = 0;
+    f->timing = getenv("BHRT_HOST_TIMING") != NULL;
+    struct timespec th[4];
+    clock_gettime(CLOCK_MONOTONIC, &th[0]);
+    if (f->timing && !f->t_ev[0]) {
+        HIP_TRY(hipSetDevice(0));
+        for (int i = 0; i < 2 + 2 * BHRT_MAX_CHUNKS; i++) HIP_TRY(hipEventCreate(&f->t_ev[i]));
+    }
     const bhrt_frame_soa fields = device_fields(host);
-    for (int d = 0; d < ndev; d++) { /* buffers: every chunk of device d */
+    for (int d = 0; d < ndev; d++) { /* device buffers: every chunk of device d */
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
         HIP_TRY(hipSetDevice(d));
-        size_t dev_bytes = 0, host_bytes = 0;
+        size_t dev_bytes = 0;
         for (int k = 0; k < K; k++) {
-            bhrt_rows* r = &rows[k][d];
+            bhrt_rows* r = &f->rows[k][d];
             r->row_block = block;
             r->shard = k * ndev + d;
             r->num_shards = shards;
-            jobs[k][d].c = c;
-            jobs[k][d].n = shards > 1 ? (long)bhrt_shard_rows(H, r) * W : (long)W * H;
-            dev_bytes += soa_bytes(&fields, jobs[k][d].n);
+            f->jobs[k][d].c = c;
+            f->jobs[k][d].n = shards > 1 ? (long)bhrt_shard_rows(H, r) * W : (long)W * H;
+            dev_bytes += soa_bytes(&fields, f->jobs[k][d].n);
         }
-        if (ensure(&c->d_soa, &c->cap_soa, dev_bytes ? dev_bytes : 256, 0)) return -1;
-        char* p = (char*)c->d_soa;
-        for (int k = 0; k < K; k++) {
-            soa_carve(&p, &fields, jobs[k][d].n, &jobs[k][d].dev);
-            stage_off[k][d] = host_bytes;
-            host_bytes += wanted_bytes(&jobs[k][d], host);
-        }
-        if (ensure(&c->h_stage, &c->cap_stage, host_bytes ? host_bytes : 64, 1)) return -1;
+        if (ensure(&c->fr[slot].d_soa, &c->fr[slot].cap_soa, dev_bytes ? dev_bytes : 256, 0))
+            return -1;
+        char* p = (char*)c->fr[slot].d_soa;
+        for (int k = 0; k < K; k++) soa_carve(&p, &fields, f->jobs[k][d].n, &f->jobs[k][d].dev);
     }
-    for (int k = 0; k < K; k++) /* trace, then queue each chunk's copy behind it */
+    if (f->timing) { /* time origin: when the frame's first chunk is queued */
+        HIP_TRY(hipSetDevice(0));
+        HIP_TRY(hipEventRecord(f->t_ev[0], (ticket & 1) ? f->jobs[0][0].c->stream2
+                                                          : f->jobs[0][0].c->stream));
+    }
+    for (int k = 0; k < K; k++) /* trace every chunk; consecutive chunks and frames alternate */
         for (int d = 0; d < ndev; d++) {
-            devctx_t* c = jobs[k][d].c;
-            hipStream_t st = (k & 1) ? c->stream2 : c->stream;
+            devctx_t* c = f->jobs[k][d].c;
+            hipStream_t st = ((k + ticket) & 1) ? c->stream2 : c->stream;
             HIP_TRY(hipSetDevice(d));
-            if (jobs[k][d].n > 0 &&
-                bhrt_render_frame_device(bh, dk, cfg, cam, W, H, shards > 1 ? &rows[k][d] : NULL,
-                                         method, flags, &jobs[k][d].dev, st))
+            if (f->jobs[k][d].n > 0 &&
+                bhrt_render_frame_device(bh, dk, cfg, cam, W, H, shards > 1 ? &f->rows[k][d] : NULL,
+                                         method, flags, &f->jobs[k][d].dev, st))
                 return -1;
-            HIP_TRY(hipEventRecord(c->chunk_done[k], st));
-            HIP_TRY(hipStreamWaitEvent(c->copy, c->chunk_done[k], 0));
-            if (readback_issue(&jobs[k][d], host, (char*)c->h_stage + stage_off[k][d], c->copy))
-                return -1;
-            HIP_TRY(hipEventRecord(c->chunk_copied[k], c->copy));
+            HIP_TRY(hipEventRecord(c->fr[slot].done[k], st));
+            if (f->timing && d == 0) HIP_TRY(hipEventRecord(f->t_ev[2 + 2 * k], st));
         }
-    for (int k = 0; k < K; k++) /* un-permute each chunk as it lands */
+    clock_gettime(CLOCK_MONOTONIC, &th[1]);
+    /* while the GPU traces: make the caller's arrays DMA-able (or fall back to staging).
+     * Small frames take the staging path: registering costs ~1 us per 4 KB page. */
+    size_t frame_bytes = 0;
+    for (int k = 0; k < BHRT_NFIELDS; k++)
+        if (*soa_slot(&f->host, k)) frame_bytes += k_fsize[k] * (size_t)W * (size_t)H;
+    f->direct = frame_bytes >= ((size_t)8 << 20) && !getenv("BHRT_HOST_STAGING") &&
+                register_host(f) == 0;
+    if (!f->direct)
         for (int d = 0; d < ndev; d++) {
-            devctx_t* c = jobs[k][d].c;
+            devctx_t* c = f->jobs[0][d].c;
+            size_t host_bytes = 0;
+            for (int k = 0; k < K; k++) {
+                f->stage_off[k][d] = host_bytes;
+                host_bytes += wanted_bytes(&f->jobs[k][d], host);
+            }
             HIP_TRY(hipSetDevice(d));
-            HIP_TRY(hipEventSynchronize(c->chunk_copied[k]));
-            readback_finish(&jobs[k][d], host, (const char*)c->h_stage + stage_off[k][d], W,
-                            shards > 1 ? &rows[k][d] : NULL);
+            if (ensure(&c->fr[slot].h_stage, &c->fr[slot].cap_stage, host_bytes ? host_bytes : 64, 1))
+                return -1;
         }
+    clock_gettime(CLOCK_MONOTONIC, &th[2]);
+    for (int k = 0; k < K; k++) /* each chunk's copy queued behind its trace */
+        for (int d = 0; d < ndev; d++) {
+            devctx_t* c = f->jobs[k][d].c;
+            HIP_TRY(hipSetDevice(d));
+            HIP_TRY(hipStreamWaitEvent(c->copy, c->fr[slot].done[k], 0));
+            const bhrt_rows* r = shards > 1 ? &f->rows[k][d] : NULL;
+            if (f->jobs[k][d].n > 0 &&
+                (f->direct ? copy_chunk_direct(&f->jobs[k][d], host, W, r, c->copy)
+                           : readback_issue(&f->jobs[k][d], host,
+                                            (char*)c->fr[slot].h_stage + f->stage_off[k][d],
+                                            c->copy))) {
+                unregister_host(f);
+                return -1;
+            }
+            HIP_TRY(hipEventRecord(c->fr[slot].copied[k], c->copy));
+            if (f->timing && d == 0) HIP_TRY(hipEventRecord(f->t_ev[3 + 2 * k], c->copy));
+        }
+    clock_gettime(CLOCK_MONOTONIC, &th[3]);
+    for (int i = 0; i < 3; i++)
+        f->t_host[i] = (th[i + 1].tv_sec - th[i].tv_sec) * 1e3 + (th[i + 1].tv_nsec - th[i].tv_nsec) * 1e-6;
+    f->active = 1;
+    if (ticket_out) *ticket_out = ticket;
     return 0;
+}
+
+int bhrt_render_frame_async(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                            const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                            IntegrationMethod method, int flags, const bhrt_frame_soa* host,
+                            int* ticket) {
+    return render_frame_issue(bh, dk, cfg, cam, W, H, method, flags, host, ticket);
+}
+
+int bhrt_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                      const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                      IntegrationMethod method, int flags, const bhrt_frame_soa* host) {
+    int ticket = 0;
+    if (render_frame_issue(bh, dk, cfg, cam, W, H, method, flags, host, &ticket)) return -1;
+    return bhrt_frame_wait(ticket);
 }
 
 int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
