@@ -466,9 +466,12 @@ def test_sub_pixel_offset_frames(bhrt_lib, oracle):
         compare(got, want, RTOL, False, f"sample {k}")
 
 
-def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch):
+@pytest.mark.parametrize("staging", ["", "1"])
+def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch, staging):
     """bhrt_render_frame traces a host-buffer frame in pipelined chunks (cyclic row-block
-    shards, copies overlapped with tracing); any chunk count gives the device frame."""
+    shards, copies overlapped with tracing); any chunk count gives the device frame, whether
+    the chunks are DMA'd into the registered caller arrays by 2-D copies (416 rows = 52 row
+    blocks: uneven shards, partial last blocks) or staged and un-permuted on the host."""
     import torch
     c = configs.CONFIGS["C2"]
     bh, dk, cfg = c.scene()
@@ -480,11 +483,82 @@ def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch):
                                  bhrt_lib.soa_from_tensors(t), 0)
     torch.cuda.synchronize()
     ref = {f: v.cpu().numpy() for f, v in t.items()}
+    monkeypatch.setenv("BHRT_HOST_STAGING", staging)
+    if not staging:
+        monkeypatch.delenv("BHRT_HOST_STAGING")
     for chunks in ("1", "3", "4", "8"):
         monkeypatch.setenv("BHRT_HOST_CHUNKS", chunks)
         got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
         for f in abi.SOA_FIELDS:
             assert np.array_equal(got[f], ref[f], equal_nan=True), (chunks, f)
+
+
+def _frame_soa_in_one_buffer(n, fields, offset=0):
+    """Caller arrays carved back to back out of ONE host allocation (fields share pages, and
+    the first starts `offset` bytes into a page): the registration must merge page ranges."""
+    sizes = [n * (16 if f == "rgba32f" else 4 if f in ("result", "steps", "rgba8") else 8)
+             for f in fields]
+    buf = np.zeros(sum(sizes) + offset + 64, dtype=np.uint8)
+    arrays, p = {}, offset
+    for f, sz in zip(fields, sizes):
+        dt = abi.SOA_DTYPES[f]
+        shape = (n, 4) if f in abi.DISPLAY_FIELDS else (n,)
+        arrays[f] = buf[p:p + sz].view(dt).reshape(shape)
+        p += sz
+    soa = abi.FrameSoA(**{f: a.ctypes.data for f, a in arrays.items()})
+    return buf, arrays, soa
+
+
+def test_async_frames_in_flight_equal_sync_frames(bhrt_lib):
+    """bhrt_render_frame_async: four frames of different scenes queued back to back (three in
+    flight, the fourth waits for the oldest slot), into separate host arrays -- one set
+    carved out of a single allocation at an odd page offset, one set page-locked by the
+    caller beforehand (hipHostRegister: used as it is, left registered) -- each equals the
+    synchronous frame; waiting twice, or for a ticket never issued, is an error."""
+    L = bhrt_lib.load()
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+    hip.hipHostUnregister.argtypes = [C.c_void_p]
+    W, H = 1024, 576  # 590 k rays, 56 MB of fields: the DMA path, 2 chunks
+    jobs = [("C2", "B"), ("C4", "B"), ("C3", "A"), ("C2", "V")]
+    outs, keep = [], []
+    for i, (cname, camname) in enumerate(jobs):
+        fields = abi.SOA_FIELDS + (abi.DISPLAY_FIELDS if i == 1 else ())
+        if i == 2:
+            buf, arrays, soa = _frame_soa_in_one_buffer(W * H, fields, offset=1000)
+            keep.append(buf)
+        else:
+            arrays, soa = abi.alloc_soa(W * H, fields)
+        outs.append((arrays, soa))
+    pre = outs[3][0]["distance"]
+    assert hip.hipHostRegister(pre.ctypes.data, pre.nbytes, 0) == 0
+    try:
+        tickets = []
+        for (cname, camname), (arrays, soa) in zip(jobs, outs):
+            c = configs.CONFIGS[cname]
+            bh, dk, cfg = c.scene()
+            t = C.c_int(0)
+            assert L.bhrt_render_frame_async(C.byref(bh), C.byref(dk) if dk else None,
+                                             C.byref(cfg), C.byref(configs.camera(camname)), W,
+                                             H, c.method, c.flags, C.byref(soa),
+                                             C.byref(t)) == 0, bhrt_lib.last_error()
+            tickets.append(t.value)
+        assert len(set(tickets)) == 4 and min(tickets) > 0
+        # the fourth issue reused the first slot: frame 1 was waited for implicitly
+        assert L.bhrt_frame_wait(tickets[0]) == -1
+        for t in tickets[1:]:
+            assert L.bhrt_frame_wait(t) == 0, bhrt_lib.last_error()
+        assert L.bhrt_frame_wait(tickets[-1]) == -1  # already waited for
+        assert L.bhrt_frame_wait(max(tickets) + 100) == -1
+    finally:
+        assert hip.hipHostUnregister(pre.ctypes.data) == 0  # still the caller's registration
+    for (cname, camname), (arrays, _) in zip(jobs, outs):
+        c = configs.CONFIGS[cname]
+        bh, dk, cfg = c.scene()
+        want = bhrt_lib.render_frame(bh, dk, cfg, configs.camera(camname), W, H, c.method,
+                                     c.flags, fields=tuple(arrays))
+        for f in arrays:
+            assert np.array_equal(arrays[f], want[f], equal_nan=True), (cname, camname, f)
 
 
 @pytest.mark.parametrize("n", [65536, 300_001, (1 << 20) + 7])  # 4, 4 and 8 chunks

@@ -1,0 +1,63 @@
+"""libbhrt's host layer on SIMULATED devices, without a GPU (multi-device state).
+
+tests/fakehip/fake_hip.c stands in for the HIP runtime with host memory tagged by device and
+synchronous streams, and aborts on a cross-device stream, event, copy or launch buffer, or on
+an asynchronous D2H copy into host memory that is neither pinned nor registered.
+tests/fakehip/multidev_driver.c stubs the trace launcher (it checks every launch buffer
+against the current device and writes an encoding of each ray's image pixel) and drives,
+from two host threads at once, frames split over two devices and several chunks (DMA into
+registered caller arrays, staged, frames in flight) and ray batches split over the devices,
+checking that every value lands at its pixel. Built twice: ASan+UBSan and TSan."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+CSRC = os.path.join(ROOT, "raytracing-engine-in-c_amd", "csrc")
+FAKE = os.path.join(ROOT, "tests", "fakehip")
+
+
+def build(tmp_path, name, sanitize, openmp):
+    exe = str(tmp_path / name)
+    cmd = ["gcc", "-std=gnu11", "-O1", "-g", f"-fsanitize={sanitize}", "-fno-omit-frame-pointer",
+           "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include",
+           "-I", os.path.join(ROOT, "include"), "-I", CSRC,
+           os.path.join(FAKE, "multidev_driver.c"), os.path.join(FAKE, "fake_hip.c"),
+           os.path.join(CSRC, "bhrt_api.c"), os.path.join(CSRC, "particles.c"),
+           os.path.join(CSRC, "kerr_helpers.c"), "-lpthread", "-lm", "-o", exe]
+    if openmp:
+        cmd.insert(1, "-fopenmp")
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return exe
+
+
+def run(exe, **env):
+    e = dict(os.environ, FAKEHIP_DEVICES="2", **env)
+    e.pop("HIP_VISIBLE_DEVICES", None)
+    r = subprocess.run([exe], capture_output=True, text=True, env=e, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-6000:]
+    assert "all checks passed" in r.stdout
+    return r
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+@pytest.mark.parametrize("staging", ["", "1"])
+def test_two_simulated_devices_asan_ubsan(tmp_path, staging):
+    exe = build(tmp_path, "multidev_asan", "address,undefined", openmp=True)
+    env = {"ASAN_OPTIONS": "detect_leaks=0", "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}
+    if staging:
+        env["BHRT_HOST_STAGING"] = "1"
+    r = run(exe, **env)
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_two_simulated_devices_tsan(tmp_path):
+    """Two host threads through the same library: per-thread contexts must not race. Built
+    without OpenMP (libgomp is not TSan-instrumented); the host copies then run serially."""
+    exe = build(tmp_path, "multidev_tsan", "thread", openmp=False)
+    r = run(exe, TSAN_OPTIONS="halt_on_error=1")
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
