@@ -314,6 +314,13 @@ int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* blackhole,
                     const AccretionDiskParams* disk, const SimulationConfig* config,
                     IntegrationMethod method, int flags, const bhrt_frame_soa* host_out);
 
+/* Diagnostic: both forms of the trace kernel's RKF45 accept test (the division-free fast
+ * form and the reference's literal quotient, geodesic.hip rkf45_accept) on n cases of DEVICE
+ * arrays err[6n], scale[6n], tol[n]; d_out[2i] / d_out[2i+1] = the two decisions. Returns 0
+ * or a hipError_t value; asynchronous on hip_stream. */
+int bhrt_check_rkf45_accept(const double* err, const double* scale, const double* tol, int n,
+                            int* out, void* hip_stream);
+
 /* Copy and optionally reset this thread's statistics (waits for the timed launches). */
 int bhrt_get_stats(bhrt_stats* out, int reset);
 

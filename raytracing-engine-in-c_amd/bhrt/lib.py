@@ -11,7 +11,8 @@ import numpy as np
 from . import abi
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("BHRT_LIB", os.path.join(_PKG_DIR, "libbhrt.so"))
+_DEFAULT_PATH = os.path.join(_PKG_DIR, "libbhrt.so")
+LIB_PATH = os.environ.get("BHRT_LIB", _DEFAULT_PATH)
 
 
 class BhrtError(RuntimeError):
@@ -97,7 +98,10 @@ def load(path=None):
     if not os.path.exists(p):
         raise BhrtError(f"libbhrt.so not built at {p} (run __graft_entry__.build())")
     lib = C.CDLL(p)
+    older = p != _DEFAULT_PATH  # an A/B build of an earlier revision may lack newer entry points
     for name, (res, args) in _PROTOS.items():
+        if older and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -375,6 +375,41 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
     }
 }
 
+// RKF45's accept test (math_util.c:367-391, 402-434): accept iff
+// RN(max_i RN(err_i / scale_i) / tol) <= 1, scale_i >= 1e-10. For a positive normal (finite)
+// tol the outer test is exactly max_error <= tol: x <= t gives x / t <= 1; x > t means
+// x >= t + ulp(t), so x / t >= 1 + ulp(t) / t > 1 + 2^-53, the rounding midpoint above 1
+// (x = Inf: Inf / t = Inf > 1, also a reject). That is, every component's RN(err / scale) <=
+// tol. FAST (where the state is provably bounded, repair_at_refill: |scale| < 2^600, so
+// 1/scale is normal) decides a component from q = err * rcp(scale), within 2^-50 of
+// err / scale: q < tol (1 - 2^-40) passes, q > tol (1 + 2^-40) rejects, and only a q inside
+// that band (per lane, rare) takes the IEEE quotient. Otherwise, and for a tol that is <= 0,
+// subnormal, Inf or NaN, the literal final quotient decides (wave-uniform branch on tol):
+// tol = Inf with max_error = Inf is Inf / Inf = NaN, a reject, where max_error <= tol would
+// accept. bhrt_check_rkf45_accept runs both forms on given operands
+// (tests/test_gpu_parity.py::test_rkf45_accept_band).
+template <bool FAST>
+__device__ __forceinline__ bool rkf45_accept(const double (&err)[6], const double (&scale)[6],
+                                             double tol) {
+    const bool tol_normal = tol >= 2.2250738585072014e-308 && tol <= 1.79769313486231570815e+308;
+    if (FAST && tol_normal) {
+        const double lo = tol * (1.0 - 0x1p-40), hi = tol * (1.0 + 0x1p-40);
+        double near_max = 0.0;
+        bool over = false;
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const double q = err[i] * rcp_nr(scale[i]);
+            over |= q > hi;
+            if (__builtin_expect(q >= lo && q <= hi, 0)) near_max = fmax(near_max, err[i] / scale[i]);
+        }
+        return !over && near_max <= tol;
+    }
+    double max_error = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) max_error = fmax(max_error, err[i] / scale[i]);
+    return tol_normal ? max_error <= tol : max_error / tol <= 1.0;
+}
+
 // rkf45_integrate (math_util.c:212-457), n = 6. Returns true on accept (y <- y5).
 template <bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Scene& sc,
@@ -417,48 +452,18 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
         yt[i] = y[i] + h * (b61 * k1[i] + b62 * k2[i] + b63 * k3[i] + b64 * k4[i] + b65 * k5[i]);
     rhs<SPIN0, FAR, HUGE>(yt, k6, sc, far_ok, n, tr, false);
     double y5[6];
-    // :367-391 and :402-434: accept iff RN(max_i RN(|y5_i - y4_i| / scale_i) / tol) <= 1.
-    // For a positive normal (finite) tol the outer test is exactly max_error <= tol: x <= t
-    // gives x / t <= 1; x > t means x >= t + ulp(t), so x / t >= 1 + ulp(t) / t > 1 + 2^-53, the
-    // rounding midpoint above 1 (x = Inf: Inf / t = Inf > 1, also a reject). That is, every
-    // component's RN(a / b) <= tol. Where the state is provably bounded (repair_at_refill:
-    // |b| < 2^600, so 1/b is normal) a component is decided from q = a * rcp(b), within 2^-50 of
-    // a / b: q < tol (1 - 2^-40) passes, q > tol (1 + 2^-40) rejects, and only a q inside that
-    // band (per lane, rare) takes the IEEE quotient. Other instantiations, and a tol that is
-    // <= 0, subnormal, Inf or NaN, keep the literal final quotient (wave-uniform branch on tol):
-    // tol = Inf with max_error = Inf is Inf / Inf = NaN, a reject, where max_error <= tol would
-    // accept.
+    // :367-391 and :402-434 (rkf45_accept)
     constexpr bool FAST_NORM = repair_at_refill<INTEGRATOR_RKF45, FAR, HUGE>();
-    const bool tol_normal = sc.tol >= 2.2250738585072014e-308 && sc.tol <= 1.79769313486231570815e+308;
-    bool accept;
-    if (FAST_NORM && tol_normal) {
-        const double lo = sc.tol * (1.0 - 0x1p-40), hi = sc.tol * (1.0 + 0x1p-40);
-        double near_max = 0.0;
-        bool over = false;
+    double err[6], scale[6];
 #pragma unroll
-        for (int i = 0; i < 6; i++) {
-            const double y4 = y[i] + h * (c1 * k1[i] + c3 * k3[i] + c4 * k4[i] + c5 * k5[i]);
-            y5[i] = y[i] + h * (d1 * k1[i] + d3 * k3[i] + d4 * k4[i] + d5 * k5[i] + d6 * k6[i]);
-            double scale = fmax(fabs(y[i]), fabs(y5[i]));
-            if (scale < kEps) scale = kEps;
-            const double a = fabs(y5[i] - y4);
-            const double q = a * rcp_nr(scale);
-            over |= q > hi;
-            if (__builtin_expect(q >= lo && q <= hi, 0)) near_max = fmax(near_max, a / scale);
-        }
-        accept = !over && near_max <= sc.tol;
-    } else {
-        double max_error = 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-            const double y4 = y[i] + h * (c1 * k1[i] + c3 * k3[i] + c4 * k4[i] + c5 * k5[i]);
-            y5[i] = y[i] + h * (d1 * k1[i] + d3 * k3[i] + d4 * k4[i] + d5 * k5[i] + d6 * k6[i]);
-            double scale = fmax(fabs(y[i]), fabs(y5[i]));
-            if (scale < kEps) scale = kEps;
-            max_error = fmax(max_error, fabs(y5[i] - y4) / scale);
-        }
-        accept = tol_normal ? max_error <= sc.tol : max_error / sc.tol <= 1.0;
+    for (int i = 0; i < 6; i++) {
+        const double y4 = y[i] + h * (c1 * k1[i] + c3 * k3[i] + c4 * k4[i] + c5 * k5[i]);
+        y5[i] = y[i] + h * (d1 * k1[i] + d3 * k3[i] + d4 * k4[i] + d5 * k5[i] + d6 * k6[i]);
+        scale[i] = fmax(fabs(y[i]), fabs(y5[i]));
+        if (scale[i] < kEps) scale[i] = kEps;
+        err[i] = fabs(y5[i] - y4);
     }
+    const bool accept = rkf45_accept<FAST_NORM>(err, scale, sc.tol);
     if (accept) {
 #pragma unroll
         for (int i = 0; i < 6; i++) y[i] = y5[i];
@@ -1201,6 +1206,23 @@ __global__ void k_path(const bhrt_kparams kp, double t0, double ox, double oy, d
     store_hit(kp.out, 0, R, term, kp.sc);
 }
 
+// Both forms of the RKF45 accept test (rkf45_accept) on given operands: case i has six
+// components err[6i..6i+5], scale[6i..6i+5] and tolerance tol[i]; out[2i] = the fast form's
+// decision, out[2i+1] = the literal quotient's.
+__global__ void k_check_accept(const double* err, const double* scale, const double* tol, int n,
+                               int* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double e[6], s[6];
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+        e[c] = err[6 * i + c];
+        s[c] = scale[6 * i + c];
+    }
+    out[2 * i] = rkf45_accept<true>(e, s, tol[i]);
+    out[2 * i + 1] = rkf45_accept<false>(e, s, tol[i]);
+}
+
 // ---- launch plumbing --------------------------------------------------------------------
 // Launch geometry is cached per device: a process may drive several devices (bhrt_render_frame
 // splits a frame over every visible one) from several host threads. Every cached value is a
@@ -1344,6 +1366,15 @@ extern "C" int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0
     case INTEGRATOR_RKF45: return dispatch_disk<INTEGRATOR_RKF45>(*kp, st, e0, e1);
     default: return dispatch_disk<INTEGRATOR_LEAPFROG>(*kp, st, e0, e1);  // no-op integrators
     }
+}
+
+extern "C" __attribute__((visibility("default"))) int bhrt_check_rkf45_accept(
+    const double* d_err, const double* d_scale, const double* d_tol, int n, int* d_out,
+    void* stream) {
+    if (n <= 0) return 0;
+    k_check_accept<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(
+        d_err, d_scale, d_tol, n, d_out);
+    return (int)hipGetLastError();
 }
 
 extern "C" int bhrt_launch_path(const bhrt_kparams* kp, const double* o4, const double* d3,

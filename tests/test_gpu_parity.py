@@ -587,3 +587,61 @@ def test_large_batch_pipelined_equals_soa_trace(bhrt_lib, n):
     for i, ax in enumerate("xyz"):
         assert np.array_equal(hits["sky_direction"][esc, i], ref["sky_" + ax][esc])
     assert not hits["sky_direction"][~esc].any()
+
+
+def test_rkf45_accept_band(bhrt_lib):
+    """The trace kernel's RKF45 accept test (geodesic.hip rkf45_accept): the
+    division-free fast form -- q = err * rcp(scale) decides outside a +-2^-40 band around
+    tol, the IEEE quotient inside it -- must make the reference's decision
+    RN(max_i RN(err_i / scale_i) / tol) <= 1 (math_util.c:376-405) exactly, including
+    quotients landing ON tol, one ulp either side, on and around the band's edges, several
+    components in the band at once, and the literal path's tolerances (0, subnormal, Inf,
+    NaN, negative). Operands are run through the kernel's own device code
+    (bhrt_check_rkf45_accept) and checked against numpy's IEEE division."""
+    import torch
+    L = bhrt_lib.load()
+    L.bhrt_check_rkf45_accept.restype = C.c_int
+    L.bhrt_check_rkf45_accept.argtypes = [C.c_void_p] * 3 + [C.c_int, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(45)
+    errs, scales, tols = [], [], []
+    rel = [0.0, 2.0 ** -40, -2.0 ** -40, 2.0 ** -41, -2.0 ** -41, 2.0 ** -39, -2.0 ** -39,
+           2.0 ** -52, -2.0 ** -52, 1e-9, -1e-9]
+    for _ in range(4000):
+        tol = 10.0 ** rng.uniform(-12, -3)
+        if rng.random() < 0.2:
+            tol = rng.choice([1e-6, 1e-8])
+        scale = np.full(6, 10.0 ** rng.uniform(-10, 3))
+        scale[rng.random(6) < 0.2] = 1e-10  # BH_EPSILON floor
+        scale *= rng.uniform(1, 2, 6)
+        err = tol * scale * 10.0 ** rng.uniform(-6, -1, 6)  # clearly accepted components
+        for c in rng.choice(6, size=rng.integers(1, 4), replace=False):
+            q = tol * (1.0 + rng.choice(rel))
+            e = q * scale[c]
+            for _ in range(int(rng.integers(-3, 4))):  # nudge a few ulps either way
+                e = np.nextafter(e, np.inf if rng.random() < 0.5 else 0.0)
+            err[c] = e
+        errs.append(err)
+        scales.append(scale)
+        tols.append(tol)
+    for t in (0.0, 5e-324, np.inf, np.nan, -1e-6, 2.2250738585072014e-308):  # literal path
+        for big in (0.0, np.inf):
+            err = np.full(6, 1e-20)
+            err[0] = big
+            errs.append(err)
+            scales.append(np.ones(6))
+            tols.append(t)
+    E, S, T = np.array(errs), np.array(scales), np.array(tols)
+    n = len(T)
+    dev = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (E.ravel(), S.ravel(), T)]
+    out = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    assert L.bhrt_check_rkf45_accept(*(d.data_ptr() for d in dev), n, out.data_ptr(),
+                                     C.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(n, 2)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        max_err = np.max(E / S, axis=1)
+        want = (max_err / T) <= 1.0
+    assert np.array_equal(got[:, 1], want.astype(np.int32)), "literal form vs numpy"
+    assert np.array_equal(got[:, 0], want.astype(np.int32)), np.nonzero(got[:, 0] != want)[0][:10]
+    near = np.abs(max_err / T - 1.0) <= 2.0 ** -39
+    assert near.sum() > 1000 and want[near].any() and (~want[near]).any()  # the band was hit
