@@ -340,11 +340,22 @@ constexpr bool repair_at_refill() {
     return (METHOD == INTEGRATOR_RK4 || METHOD == INTEGRATOR_RKF45) && !FAR && !HUGE;
 }
 
+// On the Kerr branch without the far-field one (a != 0, FAR = false) every stage's
+// accelerations d[3..5] are the literal 0 (raytracer.c:131-138), so a stage value or update of
+// components 3..5 is y + h * (sum of b * 0) = y exactly for the finite state and finite h the
+// loop has (only a zero's sign can differ: -0 + +0 = +0). Those components are carried
+// unchanged instead of computed (C5: 3 of the 6 components of every RKF45 combination).
+template <bool SPIN0, bool FAR>
+constexpr bool zero_accel() {
+    return !SPIN0 && !FAR;
+}
+
 // rk4_integrate (math_util.c:162-207) on the six live components; the running sum
 // ((k1 + 2k2) + 2k3) + k4 is the reference's left-to-right evaluation order.
 template <bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& sc, bool far_ok,
                                          Counters& n, Trig1& tr) {
+    constexpr bool Z = zero_accel<SPIN0, FAR>();
     double k[6], acc[6], yt[6];
     const double hh = 0.5 * h;
     const double h6 = h * (1.0 / 6.0);
@@ -352,26 +363,26 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         acc[i] = k[i];
-        yt[i] = y[i] + hh * k[i];
+        yt[i] = (Z && i >= 3) ? y[i] : y[i] + hh * k[i];
     }
     rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         acc[i] = acc[i] + 2.0 * k[i];
-        yt[i] = y[i] + hh * k[i];
+        yt[i] = (Z && i >= 3) ? y[i] : y[i] + hh * k[i];
     }
     rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         acc[i] = acc[i] + 2.0 * k[i];
-        yt[i] = y[i] + h * k[i];
+        yt[i] = (Z && i >= 3) ? y[i] : y[i] + h * k[i];
     }
     rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         // h * (...) / 6 as (h * RN(1/6)) * (...): the increment differs by <= 1 ulp of itself,
         // which is ~h*|k| / |y| ulp of the state
-        y[i] = __builtin_fma(h6, acc[i] + k[i], y[i]);
+        if (!(Z && i >= 3)) y[i] = __builtin_fma(h6, acc[i] + k[i], y[i]);
     }
 }
 
@@ -388,7 +399,7 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
 // tol = Inf with max_error = Inf is Inf / Inf = NaN, a reject, where max_error <= tol would
 // accept. bhrt_check_rkf45_accept runs both forms on given operands
 // (tests/test_gpu_parity.py::test_rkf45_accept_band).
-template <bool FAST>
+template <bool FAST, int NC = 6>
 __device__ __forceinline__ bool rkf45_accept(const double (&err)[6], const double (&scale)[6],
                                              double tol) {
     const bool tol_normal = tol >= 2.2250738585072014e-308 && tol <= 1.79769313486231570815e+308;
@@ -397,7 +408,7 @@ __device__ __forceinline__ bool rkf45_accept(const double (&err)[6], const doubl
         double near_max = 0.0;
         bool over = false;
 #pragma unroll
-        for (int i = 0; i < 6; i++) {
+        for (int i = 0; i < NC; i++) {  // components NC.. have err = 0 (zero_accel)
             const double q = err[i] * rcp_nr(scale[i]);
             over |= q > hi;
             if (__builtin_expect(q >= lo && q <= hi, 0)) near_max = fmax(near_max, err[i] / scale[i]);
@@ -434,22 +445,28 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
         if (bad) return false;
     }
     const double hb21 = h * b21;
+    constexpr bool Z = zero_accel<SPIN0, FAR>();  // components 3..5 stay y (zero_accel)
 #pragma unroll
-    for (int i = 0; i < 6; i++) yt[i] = y[i] + hb21 * k1[i];
+    for (int i = 0; i < 6; i++) yt[i] = (Z && i >= 3) ? y[i] : y[i] + hb21 * k1[i];
     rhs<SPIN0, FAR, HUGE>(yt, k2, sc, far_ok, n, tr, false);
 #pragma unroll
-    for (int i = 0; i < 6; i++) yt[i] = y[i] + h * (b31 * k1[i] + b32 * k2[i]);
+    for (int i = 0; i < 6; i++)
+        yt[i] = (Z && i >= 3) ? y[i] : y[i] + h * (b31 * k1[i] + b32 * k2[i]);
     rhs<SPIN0, FAR, HUGE>(yt, k3, sc, far_ok, n, tr, false);
 #pragma unroll
-    for (int i = 0; i < 6; i++) yt[i] = y[i] + h * (b41 * k1[i] + b42 * k2[i] + b43 * k3[i]);
+    for (int i = 0; i < 6; i++)
+        yt[i] = (Z && i >= 3) ? y[i] : y[i] + h * (b41 * k1[i] + b42 * k2[i] + b43 * k3[i]);
     rhs<SPIN0, FAR, HUGE>(yt, k4, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++)
-        yt[i] = y[i] + h * (b51 * k1[i] + b52 * k2[i] + b53 * k3[i] + b54 * k4[i]);
+        yt[i] = (Z && i >= 3) ? y[i]
+                              : y[i] + h * (b51 * k1[i] + b52 * k2[i] + b53 * k3[i] + b54 * k4[i]);
     rhs<SPIN0, FAR, HUGE>(yt, k5, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++)
-        yt[i] = y[i] + h * (b61 * k1[i] + b62 * k2[i] + b63 * k3[i] + b64 * k4[i] + b65 * k5[i]);
+        yt[i] = (Z && i >= 3) ? y[i]
+                              : y[i] + h * (b61 * k1[i] + b62 * k2[i] + b63 * k3[i] +
+                                            b64 * k4[i] + b65 * k5[i]);
     rhs<SPIN0, FAR, HUGE>(yt, k6, sc, far_ok, n, tr, false);
     double y5[6];
     // :367-391 and :402-434 (rkf45_accept)
@@ -457,13 +474,23 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
     double err[6], scale[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) {
+        if (Z && i >= 3) {  // y4 = y5 = y: error 0
+            y5[i] = y[i];
+            scale[i] = fmax(fabs(y[i]), kEps);
+            err[i] = 0.0;
+            continue;
+        }
         const double y4 = y[i] + h * (c1 * k1[i] + c3 * k3[i] + c4 * k4[i] + c5 * k5[i]);
         y5[i] = y[i] + h * (d1 * k1[i] + d3 * k3[i] + d4 * k4[i] + d5 * k5[i] + d6 * k6[i]);
         scale[i] = fmax(fabs(y[i]), fabs(y5[i]));
         if (scale[i] < kEps) scale[i] = kEps;
         err[i] = fabs(y5[i] - y4);
     }
-    const bool accept = rkf45_accept<FAST_NORM>(err, scale, sc.tol);
+    // a zero error passes the fast form's per-component test for any positive normal tol, so
+    // the fast form looks at the live components only; the literal form keeps all six (its
+    // fmax chain would turn an earlier NaN into the 0 of a later component, as the
+    // reference's does)
+    const bool accept = rkf45_accept<FAST_NORM, (Z && FAST_NORM) ? 3 : 6>(err, scale, sc.tol);
     if (accept) {
 #pragma unroll
         for (int i = 0; i < 6; i++) y[i] = y5[i];
@@ -727,7 +754,10 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     }
     double x, y, z;
     if (moved) {
-        trig_advance(tr.a, R.y[1], R.s1, R.c1, hc);
+        // sin, cos of state[1] feed only the a = 0 accelerations (rhs); the Kerr branch
+        // (a != 0, accelerations 0) never reads them, and the compiler keeps a dead
+        // loop-carried advance alive otherwise (C5: 45 instructions of the loop)
+        if (SPIN0) trig_advance(tr.a, R.y[1], R.s1, R.c1, hc);
         trig_advance(a2, R.y[2], R.s2, R.c2, hc);
         trig_advance(a3, R.y[3], R.s3, R.c3, hc);
     }
@@ -932,6 +962,11 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     // at least claim_min, guided scheduling) that the wave hands out over its next refills.
     // Per-wave state in LDS (touched only at refill, so it holds no registers across the
     // loop): [lo, hi) = claimed ids not yet handed out, cur = queue, moves = queues left behind.
+    // The RK4 a = 0 path (C1, C2) keeps ONE queue and claims exactly the idle lanes: its rays
+    // live up to max_steps iterations, so claims are rare (~30 M/s on C2) and the multi-queue
+    // refill block measured -2% there (its registers perturb the 4-wave hot loop; same-box
+    // A/B, profiles/r02_claim_sweep.txt).
+    constexpr bool MULTIQ = !(METHOD == INTEGRATOR_RK4 && SPIN0);
     __shared__ unsigned s_q[BHRT_TRACE_WAVES_PER_BLOCK][4];
     const unsigned ntotal = (unsigned)total;
     const unsigned qbits = HUGE ? 0u : (unsigned)kp.queue_bits;
@@ -944,78 +979,90 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             ? 32u - __builtin_clz((gridDim.x * (blockDim.x >> 6) * kp.claim_div >> qbits) - 1u | 1u)
             : 0u;
     const int wv = threadIdx.x >> 6;
-    if (lane == 0) {
+    if (MULTIQ && lane == 0) {
         s_q[wv][0] = 0u;
         s_q[wv][1] = 0u;
         s_q[wv][2] = (blockIdx.x * BHRT_TRACE_WAVES_PER_BLOCK + wv) & (nq - 1u);
         s_q[wv][3] = 0u;
     }
-    bool exhausted = false;  // every queue dry and the block handed out; wave-uniform
+    bool exhausted = false;  // no ids left to claim or hand out; wave-uniform
     const HSel hsel{kp.sc.h_far, kp.sc.h_15, kp.sc.h_5, kp.sc.h_2_5};
     for (;;) {
         const unsigned long long live_mask = __ballot(live);
         int n_live = __popcll(live_mask);
         if (!exhausted && (64 - n_live >= kp.refill || n_live == 0)) {
-            const unsigned need = 64u - (unsigned)n_live;
-            unsigned lo = __builtin_amdgcn_readfirstlane(s_q[wv][0]);
-            unsigned hi = __builtin_amdgcn_readfirstlane(s_q[wv][1]);
-            unsigned cur = __builtin_amdgcn_readfirstlane(s_q[wv][2]);
-            unsigned moves = __builtin_amdgcn_readfirstlane(s_q[wv][3]);
-            const unsigned avail = hi - lo;
-            const unsigned rank = (unsigned)__popcll(~live_mask & below);
-            unsigned q = cur, j = lo + rank;  // lanes beyond the block take ids of the new claim
-            bool ok = rank < avail;
-            if (avail >= need || moves >= nq) {
-                lo += avail >= need ? need : avail;
+            bool ok;
+            unsigned long long id;
+            if constexpr (MULTIQ) {
+                const unsigned need = 64u - (unsigned)n_live;
+                unsigned lo = __builtin_amdgcn_readfirstlane(s_q[wv][0]);
+                unsigned hi = __builtin_amdgcn_readfirstlane(s_q[wv][1]);
+                unsigned cur = __builtin_amdgcn_readfirstlane(s_q[wv][2]);
+                unsigned moves = __builtin_amdgcn_readfirstlane(s_q[wv][3]);
+                const unsigned avail = hi - lo;
+                const unsigned rank = (unsigned)__popcll(~live_mask & below);
+                unsigned q = cur, j = lo + rank;  // lanes beyond the block take ids of the new claim
+                ok = rank < avail;
+                if (avail >= need || moves >= nq) {
+                    lo += avail >= need ? need : avail;
+                } else {
+                    const unsigned want = need - avail;
+                    unsigned b = 0, e = 0;
+                    bool hopped = false;
+                    for (;;) {  // wave-uniform; at most Q - 1 hops over the wave's life
+                        const unsigned size = queue_size(ntotal, qbits, cur);
+                        unsigned long long* const hp = heads + (size_t)cur * qstride;
+                        unsigned c = want;
+                        if (kp.claim_div > 0 && !hopped) {
+                            c = ((size - hi) >> shift) + 63u & ~63u;
+                            if (c < (unsigned)kp.claim_min) c = (unsigned)kp.claim_min;
+                            if (c < want) c = want;
+                        }
+                        unsigned long long base = 0;
+                        if (lane == 0) {
+                            // a queue reached by a hop may be dry already: look before claiming
+                            if (hopped)
+                                base = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (base < size) base = atomicAdd(hp, (unsigned long long)c);
+                        }
+                        base = __shfl(base, 0);
+                        if (base < size) {
+                            b = (unsigned)base;
+                            e = base + c < size ? (unsigned)(base + c) : size;
+                            break;
+                        }
+                        if (++moves >= nq) break;
+                        cur = (cur + 1u) & (nq - 1u);
+                        hi = 0u;
+                        hopped = true;
+                    }
+                    if (!ok) {
+                        q = cur;
+                        j = b + (rank - avail);
+                        ok = j < e;
+                    }
+                    lo = b + want < e ? b + want : e;
+                    hi = e;
+                }
+                exhausted = moves >= nq && lo >= hi;
+                if (lane == 0) {
+                    s_q[wv][0] = lo;
+                    s_q[wv][1] = hi;
+                    s_q[wv][2] = cur;
+                    s_q[wv][3] = moves;
+                }
+                id = queue_ray(qbits, q, j);
             } else {
-                const unsigned want = need - avail;
-                unsigned b = 0, e = 0;
-                bool hopped = false;
-                for (;;) {  // wave-uniform; at most Q - 1 hops over the wave's life
-                    const unsigned size = queue_size(ntotal, qbits, cur);
-                    unsigned long long* const hp = heads + (size_t)cur * qstride;
-                    unsigned c = want;
-                    if (kp.claim_div > 0 && !hopped) {
-                        c = ((size - hi) >> shift) + 63u & ~63u;
-                        if (c < (unsigned)kp.claim_min) c = (unsigned)kp.claim_min;
-                        if (c < want) c = want;
-                    }
-                    unsigned long long base = 0;
-                    if (lane == 0) {
-                        // a queue reached by a hop may be dry already: look before claiming
-                        if (hopped)
-                            base = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (base < size) base = atomicAdd(hp, (unsigned long long)c);
-                    }
-                    base = __shfl(base, 0);
-                    if (base < size) {
-                        b = (unsigned)base;
-                        e = base + c < size ? (unsigned)(base + c) : size;
-                        break;
-                    }
-                    if (++moves >= nq) break;
-                    cur = (cur + 1u) & (nq - 1u);
-                    hi = 0u;
-                    hopped = true;
-                }
-                if (!ok) {
-                    q = cur;
-                    j = b + (rank - avail);
-                    ok = j < e;
-                }
-                lo = b + want < e ? b + want : e;
-                hi = e;
-            }
-            exhausted = moves >= nq && lo >= hi;
-            if (lane == 0) {
-                s_q[wv][0] = lo;
-                s_q[wv][1] = hi;
-                s_q[wv][2] = cur;
-                s_q[wv][3] = moves;
+                const int need = 64 - n_live;
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(heads, (unsigned long long)need);
+                base = __shfl(base, 0);
+                exhausted = base + (unsigned long long)need >= total;
+                id = base + __popcll(~live_mask & below);
+                ok = id < total;
             }
             if (!live) {
                 if (ok) {
-                    const unsigned id = queue_ray(qbits, q, j);
                     rid = HUGE ? kp.redo[id] : (int)id;
                     if (INL) {
                         ray_init_camera(R, kp.cam, rid);
