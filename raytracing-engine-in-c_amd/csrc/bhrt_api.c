@@ -732,12 +732,13 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
 /* ---- host-buffer frames (bhrt_render_frame[_async]) ---- */
 /* A frame is traced in K chunks per device -- cyclic row-block shards k*ndev + d of K*ndev, so
  * every chunk carries the same mix of work -- alternating between two trace streams, so a
- * chunk's workgroups fill the CUs its predecessor's tail (the longest rays) frees. While the
- * GPU traces, the host registers the caller's arrays (hipHostRegister: ~1.7 ms for a C2 frame's
- * 199 MB of touched pages), and each finished chunk is copied by DMA straight into them on the
- * copy stream: one 2-D copy per field un-permutes the row blocks, so no byte passes through
- * the CPU. Arrays that cannot be registered take pinned staging and a host un-permute at
- * wait time. DESIGN.md §4 "Host-buffer frames". */
+ * chunk's workgroups fill the CUs its predecessor's tail (the longest rays) frees. Each
+ * finished chunk is copied on the copy stream into pinned staging while later chunks trace,
+ * and un-permuted into the caller's arrays by OpenMP threads when the frame is waited for
+ * (the next frames in flight keep the GPU busy meanwhile). Opt-in (BHRT_HOST_REGISTER=1): the
+ * caller's arrays are page-locked while the GPU traces (hipHostRegister) and each chunk is
+ * DMA'd straight into them, one 2-D copy per field un-permuting the row blocks.
+ * DESIGN.md §4 "Host-buffer frames". */
 typedef struct {
     int active, ticket, ndev, K, shards, W, H, direct, nreg;
     int timing;             /* BHRT_HOST_TIMING: print where the frame's time went (device 0) */
@@ -962,12 +963,16 @@ static int render_frame_issue(const BlackHoleParams* bh, const AccretionDiskPara
             if (f->timing && d == 0) HIP_TRY(hipEventRecord(f->t_ev[2 + 2 * k], st));
         }
     clock_gettime(CLOCK_MONOTONIC, &th[1]);
-    /* while the GPU traces: make the caller's arrays DMA-able (or fall back to staging).
-     * Small frames take the staging path: registering costs ~1 us per 4 KB page. */
+    /* Opt-in (BHRT_HOST_REGISTER=1): while the GPU traces, page-lock the caller's arrays and
+     * DMA straight into them. Measured no faster than pinned staging + the OpenMP un-permute
+     * (C2: 11.5-11.9 ms per frame either way, profiles/r02_host_path.txt), and it pins pages
+     * of caller memory for the frame's flight (rounded to whole pages, neighbours included),
+     * so staging is the default. Frames under 8 MB always stage. */
     size_t frame_bytes = 0;
     for (int k = 0; k < BHRT_NFIELDS; k++)
         if (*soa_slot(&f->host, k)) frame_bytes += k_fsize[k] * (size_t)W * (size_t)H;
-    f->direct = frame_bytes >= ((size_t)8 << 20) && !getenv("BHRT_HOST_STAGING") &&
+    const char* reg_env = getenv("BHRT_HOST_REGISTER");
+    f->direct = frame_bytes >= ((size_t)8 << 20) && reg_env && atoi(reg_env) > 0 &&
                 register_host(f) == 0;
     if (!f->direct)
         for (int d = 0; d < ndev; d++) {

@@ -19,6 +19,10 @@ from bhrt import abi, configs
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-5
+# Host arrays that libbhrt page-locked (BHRT_HOST_REGISTER=1) stay allocated until the process
+# ends: the HIP runtime keeps its record of a registered range past hipHostUnregister, and a
+# later pageable copy into memory re-using that address range would follow the stale record.
+_PAGE_LOCKED = []
 
 
 @pytest.mark.parametrize("name", golden_names("frame_"))
@@ -466,12 +470,13 @@ def test_sub_pixel_offset_frames(bhrt_lib, oracle):
         compare(got, want, RTOL, False, f"sample {k}")
 
 
-@pytest.mark.parametrize("staging", ["", "1"])
-def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch, staging):
+@pytest.mark.parametrize("register", ["", "1"])
+def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch, register):
     """bhrt_render_frame traces a host-buffer frame in pipelined chunks (cyclic row-block
     shards, copies overlapped with tracing); any chunk count gives the device frame, whether
-    the chunks are DMA'd into the registered caller arrays by 2-D copies (416 rows = 52 row
-    blocks: uneven shards, partial last blocks) or staged and un-permuted on the host."""
+    the chunks are staged and un-permuted on the host (default) or DMA'd into the registered
+    caller arrays by 2-D copies (BHRT_HOST_REGISTER=1; 416 rows = 52 row blocks: uneven
+    shards, partial last blocks)."""
     import torch
     c = configs.CONFIGS["C2"]
     bh, dk, cfg = c.scene()
@@ -483,12 +488,14 @@ def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch, staging):
                                  bhrt_lib.soa_from_tensors(t), 0)
     torch.cuda.synchronize()
     ref = {f: v.cpu().numpy() for f, v in t.items()}
-    monkeypatch.setenv("BHRT_HOST_STAGING", staging)
-    if not staging:
-        monkeypatch.delenv("BHRT_HOST_STAGING")
+    monkeypatch.setenv("BHRT_HOST_REGISTER", register)
+    if not register:
+        monkeypatch.delenv("BHRT_HOST_REGISTER")
     for chunks in ("1", "3", "4", "8"):
         monkeypatch.setenv("BHRT_HOST_CHUNKS", chunks)
         got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+        if register:
+            _PAGE_LOCKED.append(got)
         for f in abi.SOA_FIELDS:
             assert np.array_equal(got[f], ref[f], equal_nan=True), (chunks, f)
 
@@ -509,12 +516,16 @@ def _frame_soa_in_one_buffer(n, fields, offset=0):
     return buf, arrays, soa
 
 
-def test_async_frames_in_flight_equal_sync_frames(bhrt_lib):
+@pytest.mark.parametrize("register", ["", "1"])
+def test_async_frames_in_flight_equal_sync_frames(bhrt_lib, monkeypatch, register):
     """bhrt_render_frame_async: four frames of different scenes queued back to back (three in
     flight, the fourth waits for the oldest slot), into separate host arrays -- one set
     carved out of a single allocation at an odd page offset, one set page-locked by the
     caller beforehand (hipHostRegister: used as it is, left registered) -- each equals the
-    synchronous frame; waiting twice, or for a ticket never issued, is an error."""
+    synchronous frame; waiting twice, or for a ticket never issued, is an error. Staged
+    (default) and DMA'd into the page-locked arrays (BHRT_HOST_REGISTER=1)."""
+    if register:
+        monkeypatch.setenv("BHRT_HOST_REGISTER", register)
     L = bhrt_lib.load()
     hip = C.CDLL("libamdhip64.so")
     hip.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
@@ -552,6 +563,7 @@ def test_async_frames_in_flight_equal_sync_frames(bhrt_lib):
         assert L.bhrt_frame_wait(max(tickets) + 100) == -1
     finally:
         assert hip.hipHostUnregister(pre.ctypes.data) == 0  # still the caller's registration
+    _PAGE_LOCKED.append((outs, keep))  # (the caller-registered `pre` array too)
     for (cname, camname), (arrays, _) in zip(jobs, outs):
         c = configs.CONFIGS[cname]
         bh, dk, cfg = c.scene()

@@ -44,12 +44,12 @@ def run(exe, **env):
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
-@pytest.mark.parametrize("staging", ["", "1"])
-def test_two_simulated_devices_asan_ubsan(tmp_path, staging):
+@pytest.mark.parametrize("register", ["", "1"])
+def test_two_simulated_devices_asan_ubsan(tmp_path, register):
     exe = build(tmp_path, "multidev_asan", "address,undefined", openmp=True)
     env = {"ASAN_OPTIONS": "detect_leaks=0", "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}
-    if staging:
-        env["BHRT_HOST_STAGING"] = "1"
+    if register:
+        env["BHRT_HOST_REGISTER"] = "1"
     r = run(exe, **env)
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
 
@@ -59,5 +59,5 @@ def test_two_simulated_devices_tsan(tmp_path):
     """Two host threads through the same library: per-thread contexts must not race. Built
     without OpenMP (libgomp is not TSan-instrumented); the host copies then run serially."""
     exe = build(tmp_path, "multidev_tsan", "thread", openmp=False)
-    r = run(exe, TSAN_OPTIONS="halt_on_error=1")
+    r = run(exe, TSAN_OPTIONS="halt_on_error=1", BHRT_HOST_REGISTER="1")
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
