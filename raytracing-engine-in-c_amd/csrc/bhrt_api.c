@@ -686,34 +686,44 @@ static int host_threads(void) {
 
 static void readback_finish(const shard_job* j, const bhrt_frame_soa* host, const char* stage,
                             int W, const bhrt_rows* rows) {
+    /* every wanted field of the chunk as pieces of <= 1 MB (one image row at a time when the
+     * rows are permuted), all copied in ONE parallel loop: a C2 chunk is ~50 MB, and a single
+     * thread moves pinned staging at ~16 GB/s, which made the copies, not the GPU, the bound of
+     * frames in flight */
     const int nthreads = host_threads();
-    const int big = (size_t)j->n * 8 >= ((size_t)1 << 22); /* >= 4 MB per double field */
     const int permute = rows && rows->num_shards > 1 && W > 0;
-    size_t off = 0;
+    const size_t piece = (size_t)1 << 20;
+    long total_pieces = 0, npieces[BHRT_NFIELDS];
+    size_t off[BHRT_NFIELDS], bytes_all = 0;
+    size_t o = 0;
     for (int f = 0; f < BHRT_NFIELDS; f++) {
+        npieces[f] = 0;
+        off[f] = o;
         if (!WANTED(j, host, f)) continue;
+        const size_t total = k_fsize[f] * (size_t)j->n;
+        npieces[f] = permute ? j->n / W : (long)((total + piece - 1) / piece);
+        total_pieces += npieces[f];
+        bytes_all += total;
+        o += total;
+    }
+    const int big = bytes_all >= ((size_t)1 << 22);
+#pragma omp parallel for schedule(static) num_threads(nthreads) if (big)
+    for (long q = 0; q < total_pieces; q++) {
+        long r = q;
+        int f = 0;
+        while (r >= npieces[f]) r -= npieces[f++];
         char* dst = (char*)*soa_slot((bhrt_frame_soa*)host, f);
-        const char* src = stage + off;
+        const char* src = stage + off[f];
         const size_t fs = k_fsize[f];
-        if (permute) { /* whole rows; local row r is image row g */
+        if (permute) { /* local row r is image row g */
             const size_t row_bytes = fs * (size_t)W;
-            const long nrow = j->n / W, B = rows->row_block, S = rows->num_shards,
-                       sh = rows->shard;
-#pragma omp parallel for schedule(static) num_threads(nthreads) if (big)
-            for (long r = 0; r < nrow; r++) {
-                const long g = ((r / B) * S + sh) * B + r % B;
-                memcpy(dst + row_bytes * (size_t)g, src + row_bytes * (size_t)r, row_bytes);
-            }
-        } else { /* one contiguous block, copied in pieces */
-            const size_t total = fs * (size_t)j->n, piece = (size_t)1 << 20;
-            const long npieces = (long)((total + piece - 1) / piece);
-#pragma omp parallel for schedule(static) num_threads(nthreads) if (big)
-            for (long q = 0; q < npieces; q++) {
-                const size_t a = piece * (size_t)q, len = total - a < piece ? total - a : piece;
-                memcpy(dst + a, src + a, len);
-            }
+            const long B = rows->row_block, S = rows->num_shards, sh = rows->shard;
+            const long g = ((r / B) * S + sh) * B + r % B;
+            memcpy(dst + row_bytes * (size_t)g, src + row_bytes * (size_t)r, row_bytes);
+        } else {
+            const size_t total = fs * (size_t)j->n, a0 = piece * (size_t)r;
+            memcpy(dst + a0, src + a0, total - a0 < piece ? total - a0 : piece);
         }
-        off += fs * (size_t)j->n;
     }
 }
 
@@ -964,10 +974,12 @@ static int render_frame_issue(const BlackHoleParams* bh, const AccretionDiskPara
         }
     clock_gettime(CLOCK_MONOTONIC, &th[1]);
     /* Opt-in (BHRT_HOST_REGISTER=1): while the GPU traces, page-lock the caller's arrays and
-     * DMA straight into them. Measured no faster than pinned staging + the OpenMP un-permute
-     * (C2: 11.5-11.9 ms per frame either way, profiles/r02_host_path.txt), and it pins pages
-     * of caller memory for the frame's flight (rounded to whole pages, neighbours included),
-     * so staging is the default. Frames under 8 MB always stage. */
+     * DMA straight into them. It saves the last chunk's host copy of a synchronous frame (C2:
+     * 11.0-11.7 vs 12.3-12.9 ms) but is slower with frames in flight (10.3 vs 9.8 ms per
+     * frame), and it pins caller pages -- rounded to whole pages, neighbours included -- for
+     * the frame's flight, with the HIP runtime keeping its record of a registered range past
+     * hipHostUnregister (profiles/r02_host_path.txt), so staging is the default. Frames under
+     * 8 MB always stage. */
     size_t frame_bytes = 0;
     for (int k = 0; k < BHRT_NFIELDS; k++)
         if (*soa_slot(&f->host, k)) frame_bytes += k_fsize[k] * (size_t)W * (size_t)H;
