@@ -759,7 +759,9 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
         // loop-carried advance alive otherwise (C5: 45 instructions of the loop)
         if (SPIN0) trig_advance(tr.a, R.y[1], R.s1, R.c1, hc);
         trig_advance(a2, R.y[2], R.s2, R.c2, hc);
-        trig_advance(a3, R.y[3], R.s3, R.c3, hc);
+        // on the zero-acceleration Kerr paths state[3] never changes (zero_accel): its sin,
+        // cos stay as they are
+        if (!zero_accel<SPIN0, FAR>()) trig_advance(a3, R.y[3], R.s3, R.c3, hc);
     }
     sph2cart_t(R.y[1], R.s2, R.c2, R.s3, R.c3, x, y, z);
     const double ox = R.px, oy = R.py, oz = R.pz;
