@@ -1342,9 +1342,12 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
     // camera rays set up inside k_trace where rays are short-lived: scenes with a disk (most
     // rays end on it within tens of iterations: C4 +6.6%, C3 +16.5%) except the a = 0 RK4 path
     // (C2: lifetimes up to max_steps, refills rare; its hot blocks must fit the 4-wave 128-VGPR
-    // cap). Without a disk (C5: rays run ~40 RKF45 attempts to max_distance) it measured 5%
-    // slower (profiles/r01_ab_v10.txt).
-    constexpr bool CAN_INL = DISK && !(METHOD == INTEGRATOR_RK4 && SPIN0);
+    // cap), and the Kerr RKF45 path without a disk (C5: 51 attempts per ray since v21's cheaper
+    // attempts, so k_init's 168-byte table -- 0.7 GB written and read per 8K shard -- outweighs
+    // the set-up: +1.5% same-box, profiles/r02_ab_v20_occupancy.txt; it lost 5% on round 1's
+    // 193-attempt slab, r01_ab_v10.txt).
+    constexpr bool CAN_INL = DISK ? !(METHOD == INTEGRATOR_RK4 && SPIN0)
+                                  : (METHOD == INTEGRATOR_RKF45 && !SPIN0);
     const bool inl = CAN_INL && kp.src == BHRT_SRC_CAMERA && fabs(kp.cam.r0) < 1048576.0;
     if (inl)
         ;
