@@ -334,6 +334,20 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
             pending.append(issue(i))
         wait(pending.pop(0))
     dta = (time.perf_counter() - t0) / frames
+    # the reference's batch API (trace_rays_batch: Ray[] in, 160-byte RayTraceHit[] out, only
+    # the fields trace_ray writes) on the frame's camera rays, arrays reused
+    batch = None
+    if c.method == abi.INTEGRATOR_RK4:  # (trace_rays_batch is trace_ray, RK4)
+        rays = configs.camera_rays(cam, W, H)
+        hits = np.zeros(W * H, dtype=abi.HIT_DTYPE)
+        bargs = (rays.ctypes.data, W * H, C.byref(bh), C.byref(dk) if dk else None, C.byref(cfg),
+                 hits.ctypes.data, 0)
+        if L.trace_rays_batch(*bargs) != 0:
+            raise RuntimeError(lib.last_error())
+        t0 = time.perf_counter()
+        for _ in range(3):
+            L.trace_rays_batch(*bargs)
+        batch = round(W * H / ((time.perf_counter() - t0) / 3) / 1e6, 3)
     # one drop-in trace_ray call (the camera's forward ray), host round trip included
     ray = abi.Ray(cam.position, cam.direction)
     hit = abi.RayTraceHit()
@@ -348,10 +362,13 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
             "async_mrays_s": round(W * H / dta / 1e6, 3),
             "async_ms_per_frame": round(dta * 1e3, 3),
             "bytes_to_host_per_frame": W * H * 96,
+            "trace_rays_batch_mrays_s": batch,
             "trace_ray_latency_ms": round(sorted(lat[2:])[len(lat[2:]) // 2] * 1e3, 3),
-            "note": "bhrt_render_frame into reused host arrays (every field; DMA straight into "
-                    "the page-locked arrays); async = bhrt_render_frame_async with three frames "
-                    "in flight; trace_ray = median of one drop-in call, PCIe round trip included"}
+            "note": "bhrt_render_frame into reused host arrays (every field; pinned staging, "
+                    "host un-permute by 8 threads); async = bhrt_render_frame_async with three frames "
+                    "in flight; trace_rays_batch = the reference batch API on the frame's camera "
+                    "rays (RayTraceHit[] out); trace_ray = median of one drop-in call, PCIe "
+                    "round trip included"}
 
 
 def dist_frame_rgb():

@@ -24,6 +24,33 @@ def camera(name="B"):
     return abi.Camera(abi.v3(*c["position"]), abi.v3(*c["direction"]), abi.v3(*c["up"]), c["fov"])
 
 
+def camera_rays(cam, width, height):
+    """Pixel-centre rays of a camera frame as a Ray array (abi.RAY_DTYPE), row 0 = top: the
+    camera basis and pixel mapping of calculate_ray_direction (raytracer.c:999-1039), in numpy
+    -- synthetic input for the ray-array APIs (bench.py's trace_rays_batch leg)."""
+    import numpy as np
+
+    def norm(v):
+        n = np.sqrt((v[..., 0] * v[..., 0] + v[..., 1] * v[..., 1]) + v[..., 2] * v[..., 2])
+        return v * (1.0 / n)[..., None]
+
+    d = np.array([cam.direction.x, cam.direction.y, cam.direction.z])
+    up0 = np.array([cam.up.x, cam.up.y, cam.up.z])
+    fwd = norm(d)
+    right = norm(np.cross(fwd, up0))
+    up = np.cross(right, fwd)
+    plane_h = 2.0 * math.tan(cam.fov_deg * math.pi / 180.0 / 2.0)
+    plane_w = plane_h * (width / height)
+    px = (2.0 * ((np.arange(width) + 0.5) / width) - 1.0) * plane_w
+    py = (1.0 - 2.0 * ((np.arange(height) + 0.5) / height)) * plane_h
+    v = (fwd[None, None, :] + right[None, None, :] * px[None, :, None]) + \
+        up[None, None, :] * py[:, None, None]
+    rays = np.zeros(width * height, dtype=abi.RAY_DTYPE)
+    rays["origin"] = (cam.position.x, cam.position.y, cam.position.z)
+    rays["direction"] = norm(v).reshape(-1, 3)
+    return rays
+
+
 def row_block_for(height, shards):
     """Rows per cyclic block: the largest B <= 8 that splits `height` into `shards` equal
     shards of whole blocks (C5: 4320 rows / 8 shards -> B = 6, 540 rows each), else 8 (the

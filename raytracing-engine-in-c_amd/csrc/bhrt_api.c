@@ -1137,7 +1137,11 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
         set_err("no HIP device available (libbhrt has no CPU path)");
         return -1;
     }
-    const int K = (long)n / ndev >= (1L << 20) ? 8 : 4;
+    /* chunks per device: as for frames (frame_chunks), each chunk's copy and pack overlap the
+     * next chunk's tracing; BHRT_HOST_CHUNKS overrides */
+    int K = (long)n / ndev >= (1L << 20) ? 4 : 2;
+    const char* env = getenv("BHRT_HOST_CHUNKS");
+    if (env && atoi(env) >= 1 && atoi(env) <= BHRT_MAX_CHUNKS) K = atoi(env);
     long base[BHRT_MAX_CHUNKS + 1][BHRT_MAX_DEV]; /* chunk k of device d: [base[k][d], base[k+1][d]) */
     shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
     for (int d = 0; d < ndev; d++) {

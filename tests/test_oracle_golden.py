@@ -181,3 +181,23 @@ def test_camera_restatement_pinned_by_trace_pixel(oracle):
         assert f["result"][i] == int(res)
         if int(res) != abi.RAY_DISK:
             np.testing.assert_array_equal([f["rgb_r"][i], f["rgb_g"][i], f["rgb_b"][i]], [r, gg, b])
+
+
+def test_numpy_camera_rays_match_the_oracle(oracle):
+    """configs.camera_rays (bench.py's synthetic Ray[] input) follows calculate_ray_direction:
+    checked against the oracle's restatement on a pixel sample of every camera."""
+    import ctypes as C
+    from bhrt import abi, configs
+    O = oracle.lib
+    O.orc_camera_ray_direction.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, C.c_int,
+                                           C.c_int, C.POINTER(abi.Camera), C.POINTER(abi.Vector3D)]
+    W, H = 320, 180
+    for name in ("A", "B", "V"):
+        cam = configs.camera(name)
+        rays = configs.camera_rays(cam, W, H)
+        d = abi.Vector3D()
+        for y in range(0, H, 17):
+            for x in range(0, W, 23):
+                O.orc_camera_ray_direction(x, y, 0.5, 0.5, W, H, C.byref(cam), C.byref(d))
+                got = rays["direction"][y * W + x]
+                assert np.allclose(got, (d.x, d.y, d.z), rtol=0, atol=1e-15), (name, x, y)
