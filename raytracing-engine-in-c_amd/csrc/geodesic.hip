@@ -925,6 +925,13 @@ __device__ __forceinline__ unsigned queue_size(unsigned ntotal, unsigned qbits, 
 #define BHRT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, 256), \
                                          amdgpu_waves_per_eu(trace_waves<METHOD, DISK, SPIN0>() > 0 ? trace_waves<METHOD, DISK, SPIN0>() : 1)))
 
+// Loop iterations per trip of the persistent loop (the HUGE redo pass keeps one): RK4 6,
+// RKF45 2, from same-box sweeps of 1..8 (profiles/r02_ab_unroll.txt).
+template <int METHOD, bool SPIN0, bool HUGE>
+constexpr int unroll_n() {
+    return HUGE ? 1 : (METHOD == INTEGRATOR_RK4 ? 6 : 2);
+}
+
 // Persistent trace kernel: grid = what is resident; each wave refills idle lanes from the
 // global queue kp.ctl[0] (one returning atomic per refill).
 // FAR: some ray may take ray_derivatives' weak-field branch (origin beyond 15 rs). A camera
@@ -1097,7 +1104,14 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             continue;
         }
         if (live) {
-            const int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, &hsel);
+            int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, &hsel);
+            // further iterations in the same trip for rays that go on: the loop's hand-over
+            // copies between iterations (state, point, distance, carried sin/cos) fold away. A
+            // lane's iterations are the same either way; only its refill point moves.
+#pragma unroll
+            for (int u = 1; u < unroll_n<METHOD, SPIN0, HUGE>(); u++)
+                if (term == T_NONE && !n.huge)
+                    term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, &hsel);
             if (METHOD == INTEGRATOR_RK4 && (term != T_NONE || (!HUGE && n.huge)))
                 n.iters += R.k;  // every RK4 iteration moves, so R.k = iterations executed
             if (!HUGE && n.huge) {  // hand the ray to the HUGE instantiation
