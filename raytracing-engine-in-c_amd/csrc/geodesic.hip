@@ -350,11 +350,39 @@ constexpr bool zero_accel() {
     return !SPIN0 && !FAR;
 }
 
+// There, moreover, the stage derivatives of components 0..2 are state[3..5] -- constant over a
+// ray's life where the recovery runs once, at refill -- in every stage of every iteration, so
+// the weighted stage sums of the step's final combination are per-ray constants: formed once at
+// refill (zero_sums, the same expressions on the same values, so bit-identical), and each
+// iteration's update of components 0..2 is y + h * sum. RKF45 (C5, two 6-term sums per
+// component): +7.5% same-box; RK4 (C4, one 4-term sum, already shared by the iterations of a
+// trip) loses 1.5%, so it keeps the inline form (profiles/r02_ab_v24.txt).
+template <int METHOD, bool SPIN0, bool FAR, bool HUGE>
+constexpr bool hoist_sums() {
+    return METHOD == INTEGRATOR_RKF45 && zero_accel<SPIN0, FAR>() &&
+           repair_at_refill<METHOD, FAR, HUGE>();
+}
+
+// The step's stage sums (math_util.c:162-207, 367-391), one expression each so that the
+// hoisted and the inline forms compile to the same operations.
+__device__ __forceinline__ double rk4_acc(double acc, double k) { return acc + 2.0 * k; }
+constexpr double kC1 = 25.0 / 216.0, kC3 = 1408.0 / 2565.0, kC4 = 2197.0 / 4104.0,
+                 kC5 = -1.0 / 5.0;
+constexpr double kD1 = 16.0 / 135.0, kD3 = 6656.0 / 12825.0, kD4 = 28561.0 / 56430.0,
+                 kD5 = -9.0 / 50.0, kD6 = 2.0 / 55.0;
+__device__ __forceinline__ double rkf45_sum4(double k1, double k3, double k4, double k5) {
+    return kC1 * k1 + kC3 * k3 + kC4 * k4 + kC5 * k5;
+}
+__device__ __forceinline__ double rkf45_sum5(double k1, double k3, double k4, double k5,
+                                             double k6) {
+    return kD1 * k1 + kD3 * k3 + kD4 * k4 + kD5 * k5 + kD6 * k6;
+}
+
 // rk4_integrate (math_util.c:162-207) on the six live components; the running sum
 // ((k1 + 2k2) + 2k3) + k4 is the reference's left-to-right evaluation order.
-template <bool SPIN0, bool FAR, bool HUGE>
+template <bool SPIN0, bool FAR, bool HUGE, bool HS = false>
 __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& sc, bool far_ok,
-                                         Counters& n, Trig1& tr) {
+                                         Counters& n, Trig1& tr, const double* zs = nullptr) {
     constexpr bool Z = zero_accel<SPIN0, FAR>();
     double k[6], acc[6], yt[6];
     const double hh = 0.5 * h;
@@ -368,13 +396,13 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
     rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
-        acc[i] = acc[i] + 2.0 * k[i];
+        acc[i] = rk4_acc(acc[i], k[i]);
         yt[i] = (Z && i >= 3) ? y[i] : y[i] + hh * k[i];
     }
     rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
 #pragma unroll
     for (int i = 0; i < 6; i++) {
-        acc[i] = acc[i] + 2.0 * k[i];
+        acc[i] = rk4_acc(acc[i], k[i]);
         yt[i] = (Z && i >= 3) ? y[i] : y[i] + h * k[i];
     }
     rhs<SPIN0, FAR, HUGE>(yt, k, sc, far_ok, n, tr, false);
@@ -382,7 +410,10 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
     for (int i = 0; i < 6; i++) {
         // h * (...) / 6 as (h * RN(1/6)) * (...): the increment differs by <= 1 ulp of itself,
         // which is ~h*|k| / |y| ulp of the state
-        if (!(Z && i >= 3)) y[i] = __builtin_fma(h6, acc[i] + k[i], y[i]);
+        if (HS && i < 3)
+            y[i] = __builtin_fma(h6, zs[i], y[i]);
+        else if (!(Z && i >= 3))
+            y[i] = __builtin_fma(h6, acc[i] + k[i], y[i]);
     }
 }
 
@@ -391,10 +422,11 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
 // tol the outer test is exactly max_error <= tol: x <= t gives x / t <= 1; x > t means
 // x >= t + ulp(t), so x / t >= 1 + ulp(t) / t > 1 + 2^-53, the rounding midpoint above 1
 // (x = Inf: Inf / t = Inf > 1, also a reject). That is, every component's RN(err / scale) <=
-// tol. FAST (where the state is provably bounded, repair_at_refill: |scale| < 2^600, so
-// 1/scale is normal) decides a component from q = err * rcp(scale), within 2^-50 of
-// err / scale: q < tol (1 - 2^-40) passes, q > tol (1 + 2^-40) rejects, and only a q inside
-// that band (per lane, rare) takes the IEEE quotient. Otherwise, and for a tol that is <= 0,
+// tol. FAST (where the state is provably bounded, repair_at_refill: |scale| < 2^600) with tol
+// in [2^-900, 2^300] decides a component without a division: err <= RN(tol (1 - 2^-40) scale)
+// passes, err > RN(tol (1 + 2^-40) scale) rejects, and only an err inside that band (per lane,
+// rare) takes the IEEE quotient (v24; v17-v23 formed q = err * rcp(scale) and compared it with
+// the same band, 4 more VALU per component). Otherwise, and for a tol that is <= 0,
 // subnormal, Inf or NaN, the literal final quotient decides (wave-uniform branch on tol):
 // tol = Inf with max_error = Inf is Inf / Inf = NaN, a reject, where max_error <= tol would
 // accept. bhrt_check_rkf45_accept runs both forms on given operands
@@ -403,15 +435,20 @@ template <bool FAST, int NC = 6>
 __device__ __forceinline__ bool rkf45_accept(const double (&err)[6], const double (&scale)[6],
                                              double tol) {
     const bool tol_normal = tol >= 2.2250738585072014e-308 && tol <= 1.79769313486231570815e+308;
-    if (FAST && tol_normal) {
+    if (FAST && tol >= 0x1p-900 && tol <= 0x1p300) {
+        // tol * scale is a normal product here (scale in [1e-10, 2^600]), so RN(lo * scale) and
+        // RN(hi * scale) are within 2^-53 of the exact products
         const double lo = tol * (1.0 - 0x1p-40), hi = tol * (1.0 + 0x1p-40);
         double near_max = 0.0;
         bool over = false;
 #pragma unroll
         for (int i = 0; i < NC; i++) {  // components NC.. have err = 0 (zero_accel)
-            const double q = err[i] * rcp_nr(scale[i]);
-            over |= q > hi;
-            if (__builtin_expect(q >= lo && q <= hi, 0)) near_max = fmax(near_max, err[i] / scale[i]);
+            // err <= RN(lo s): err / s < tol (1 - 2^-41), so RN(err / s) <= tol;
+            // err > RN(hi s): err / s > tol (1 + 2^-41) > tol + ulp(tol) / 2, a reject
+            const bool pass = err[i] <= lo * scale[i];
+            const bool fail = err[i] > hi * scale[i];
+            over |= fail;
+            if (__builtin_expect(!pass && !fail, 0)) near_max = fmax(near_max, err[i] / scale[i]);
         }
         return !over && near_max <= tol;
     }
@@ -422,9 +459,10 @@ __device__ __forceinline__ bool rkf45_accept(const double (&err)[6], const doubl
 }
 
 // rkf45_integrate (math_util.c:212-457), n = 6. Returns true on accept (y <- y5).
-template <bool SPIN0, bool FAR, bool HUGE>
+template <bool SPIN0, bool FAR, bool HUGE, bool HS = false>
 __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Scene& sc,
-                                              bool far_ok, Counters& n, Trig1& tr) {
+                                              bool far_ok, Counters& n, Trig1& tr,
+                                              const double* zs = nullptr) {
     constexpr double b21 = 1.0 / 4.0;
     constexpr double b31 = 3.0 / 32.0, b32 = 9.0 / 32.0;
     constexpr double b41 = 1932.0 / 2197.0, b42 = -7200.0 / 2197.0, b43 = 7296.0 / 2197.0;
@@ -432,10 +470,6 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
                      b54 = -845.0 / 4104.0;
     constexpr double b61 = -8.0 / 27.0, b62 = 2.0, b63 = -3544.0 / 2565.0,
                      b64 = 1859.0 / 4104.0, b65 = -11.0 / 40.0;
-    constexpr double c1 = 25.0 / 216.0, c3 = 1408.0 / 2565.0, c4 = 2197.0 / 4104.0,
-                     c5 = -1.0 / 5.0;
-    constexpr double d1 = 16.0 / 135.0, d3 = 6656.0 / 12825.0, d4 = 28561.0 / 56430.0,
-                     d5 = -9.0 / 50.0, d6 = 2.0 / 55.0;
     double k1[6], k2[6], k3[6], k4[6], k5[6], k6[6], yt[6];
     rhs<SPIN0, FAR, HUGE>(y, k1, sc, far_ok, n, tr, true);
     if (!repair_at_refill<INTEGRATOR_RKF45, FAR, HUGE>()) {
@@ -480,8 +514,10 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
             err[i] = 0.0;
             continue;
         }
-        const double y4 = y[i] + h * (c1 * k1[i] + c3 * k3[i] + c4 * k4[i] + c5 * k5[i]);
-        y5[i] = y[i] + h * (d1 * k1[i] + d3 * k3[i] + d4 * k4[i] + d5 * k5[i] + d6 * k6[i]);
+        const double s4 = HS ? zs[i] : rkf45_sum4(k1[i], k3[i], k4[i], k5[i]);
+        const double s5 = HS ? zs[3 + i] : rkf45_sum5(k1[i], k3[i], k4[i], k5[i], k6[i]);
+        const double y4 = y[i] + h * s4;
+        y5[i] = y[i] + h * s5;
         scale[i] = fmax(fabs(y[i]), fabs(y5[i]));
         if (scale[i] < kEps) scale[i] = kEps;
         err[i] = fabs(y5[i] - y4);
@@ -548,9 +584,28 @@ struct Ray_ {
     double px, py, pz;  // current Cartesian position; the disk hit point once T_DISK
     double dist;
     double s1, c1, s2, c2, s3, c3;  // sin, cos of y[1], y[2], y[3] (carried)
+    double zs[6];       // per-ray stage sums of components 0..2 (hoist_sums)
     int k;              // iterations executed
     bool far_ok;        // use_analytic_approx && impact_parameter > 0
 };
+
+// hoist_sums: the stage sums of components 0..2 from the ray's constant state[3..5]
+template <int METHOD>
+__device__ __forceinline__ void zero_sums(Ray_& R) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const double v = R.y[3 + i];
+        if (METHOD == INTEGRATOR_RK4) {
+            double a = v;
+            a = rk4_acc(a, v);
+            a = rk4_acc(a, v);
+            R.zs[i] = a + v;
+        } else {
+            R.zs[i] = rkf45_sum4(v, v, v, v);
+            R.zs[3 + i] = rkf45_sum5(v, v, v, v, v);
+        }
+    }
+}
 
 __device__ __forceinline__ void trig_anchor(Ray_& R, Counters* hc = nullptr) {
     bhrt_sincos(R.y[1], &R.s1, &R.c1, hc);
@@ -745,10 +800,11 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     if (METHOD != INTEGRATOR_RK4) n.iters++;  // RK4: counted at termination (k_trace)
     Trig1 tr{R.y[1], R.s1, R.c1};
     const double a2 = R.y[2], a3 = R.y[3];
+    constexpr bool HS = hoist_sums<METHOD, SPIN0, FAR, HUGE>();
     if (METHOD == INTEGRATOR_RK4) {
-        rk4_step<SPIN0, FAR, HUGE>(R.y, h, sc, R.far_ok, n, tr);
+        rk4_step<SPIN0, FAR, HUGE, HS>(R.y, h, sc, R.far_ok, n, tr, R.zs);
     } else if (METHOD == INTEGRATOR_RKF45) {
-        moved = rkf45_attempt<SPIN0, FAR, HUGE>(R.y, h, sc, R.far_ok, n, tr);
+        moved = rkf45_attempt<SPIN0, FAR, HUGE, HS>(R.y, h, sc, R.far_ok, n, tr, R.zs);
     } else {
         moved = false;  // LEAPFROG / YOSHIDA: "not implemented", state unchanged (:616-624)
     }
@@ -901,13 +957,14 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 //    peak (160) sits in the rare-lane blocks (literal accelerations, wide trig shifts,
 //    stores). Capped at 128 the allocator spills only inside those blocks -- the hot blocks
 //    are instruction-for-instruction the 3-wave code -- so C2 gains the 4th wave (+4.6%).
-//  * RKF45, a != 0, no disk (C5): 5. With the division-free error norm the 6-wave cap spills
-//    in the hot blocks and 5 waves is best (+4.2% over 6).
+//  * RKF45, a != 0, no disk (C5): 4. Since v23's two attempts per loop trip, 5 waves spill
+//    (96 VGPRs + 156 B scratch) and 4 waves is best: +8.5% over 5, 6 loses 27%
+//    (profiles/r02_ab_v23_occupancy.txt).
 //  * C3 (RKF45 a = 0 disk) and C4 (RK4 Kerr disk) keep the compiler's choice: forcing one
 //    more wave spills in their hot blocks (-14%, -1.5%).
 template <int METHOD, bool DISK, bool SPIN0>
 constexpr int trace_waves() {
-    return (METHOD == INTEGRATOR_RKF45 && !DISK && !SPIN0) ? 5
+    return (METHOD == INTEGRATOR_RKF45 && !DISK && !SPIN0) ? 4
          : (METHOD == INTEGRATOR_RK4 && SPIN0) ? 4
          : 0;
 }
@@ -1089,6 +1146,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     // so only the velocities can need it and the origin's sin/cos stay valid
                     if (repair_at_refill<METHOD, FAR, HUGE>() && kp.sc.max_steps > 0)
                         state_repair<!INL>(R, &n);
+                    if (hoist_sums<METHOD, SPIN0, FAR, HUGE>()) zero_sums<METHOD>(R);
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
