@@ -103,8 +103,20 @@ def parse():
 # 3 velocity components it feeds (y + h * sum(b * 0)) are not work: each stage that is NOT a
 # Kerr stage adds its share of those (96 / 2 / 4 = 12 per RK4 stage, 347 / 2 / 6 = 29 per
 # RKF45 stage); the other half stays in the per-iteration base (69 and 194).
+# Where EVERY stage is a Kerr stage (a != 0 without the far-field branch: C4, C5), the stage
+# derivatives of components 0..2 are the ray's constant velocities, so their stage states are
+# never read and their weighted stage sums are per-ray constants: only what each iteration
+# must form from them is credited -- y + h * sum per component (2 ops; RKF45: y4 and y5, 4),
+# RKF45's error, scale and quotient (7 per component) -- plus the 21 ops outside the
+# components: 27 per RK4 iteration, 54 per RKF45 attempt.
+ZERO_ACCEL_OPS = {False: 27, True: 54}
+
+
 def flops(st, method):
     rkf = method == abi.INTEGRATOR_RKF45
+    per_iter = 6 if rkf else 4
+    if st["iterations"] > 0 and st["stages_kerr"] == per_iter * st["iterations"]:
+        return ZERO_ACCEL_OPS[rkf] * st["iterations"]
     base, per_live_stage = (194, 29) if rkf else (69, 12)
     live = st["stages_full"] + st["stages_far"]
     return (base * st["iterations"] + per_live_stage * live + 35 * st["stages_full"] +
