@@ -377,7 +377,7 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
             "trace_rays_batch_mrays_s": batch,
             "trace_ray_latency_ms": round(sorted(lat[2:])[len(lat[2:]) // 2] * 1e3, 3),
             "note": "bhrt_render_frame into reused host arrays (every field; pinned staging, "
-                    "host un-permute by 8 threads); async = bhrt_render_frame_async with three frames "
+                    "host un-permute by up to 16 threads); async = bhrt_render_frame_async with three frames "
                     "in flight; trace_rays_batch = the reference batch API on the frame's camera "
                     "rays (RayTraceHit[] out); trace_ray = median of one drop-in call, PCIe "
                     "round trip included"}
