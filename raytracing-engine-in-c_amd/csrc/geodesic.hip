@@ -82,6 +82,12 @@ __device__ __forceinline__ double max_raw(double a, double b) {
     asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "s"(b));
     return r;
 }
+// max(|a|, |b|) as ONE v_max_f64 with both abs modifiers (non-NaN a, b)
+__device__ __forceinline__ double max_abs_raw(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 // sin and cos of one argument, for the trace loop. OCML's sincos
 // spends ~78 VALU per call on a range reduction valid to 2^30+; every argument here (the
@@ -426,7 +432,8 @@ __device__ __forceinline__ void rk4_step(double (&y)[6], double h, const Scene& 
 // in [2^-900, 2^300] decides a component without a division: err <= RN(tol (1 - 2^-40) scale)
 // passes, err > RN(tol (1 + 2^-40) scale) rejects, and only an err inside that band (per lane,
 // rare) takes the IEEE quotient (v24; v17-v23 formed q = err * rcp(scale) and compared it with
-// the same band, 4 more VALU per component). Otherwise, and for a tol that is <= 0,
+// the same band, 4 more VALU per component; v25 first tries the one-sided test alone, which
+// accepts when every component passes it: one product and one compare per component). Otherwise, and for a tol that is <= 0,
 // subnormal, Inf or NaN, the literal final quotient decides (wave-uniform branch on tol):
 // tol = Inf with max_error = Inf is Inf / Inf = NaN, a reject, where max_error <= tol would
 // accept. bhrt_check_rkf45_accept runs both forms on given operands
@@ -439,6 +446,12 @@ __device__ __forceinline__ bool rkf45_accept(const double (&err)[6], const doubl
         // tol * scale is a normal product here (scale in [1e-10, 2^600]), so RN(lo * scale) and
         // RN(hi * scale) are within 2^-53 of the exact products
         const double lo = tol * (1.0 - 0x1p-40), hi = tol * (1.0 + 0x1p-40);
+        // every component clearly inside tol (the usual case): accept with one product and
+        // one compare per component; otherwise the two-sided test below
+        bool all_pass = true;
+#pragma unroll
+        for (int i = 0; i < NC; i++) all_pass &= err[i] <= lo * scale[i];
+        if (__builtin_expect(all_pass, 1)) return true;
         double near_max = 0.0;
         bool over = false;
 #pragma unroll
@@ -518,8 +531,14 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
         const double s5 = HS ? zs[3 + i] : rkf45_sum5(k1[i], k3[i], k4[i], k5[i], k6[i]);
         const double y4 = y[i] + h * s4;
         y5[i] = y[i] + h * s5;
-        scale[i] = fmax(fabs(y[i]), fabs(y5[i]));
-        if (scale[i] < kEps) scale[i] = kEps;
+        if (FAST_NORM) {
+            // the state is finite and bounded here (repair_at_refill), so y and y5 are not NaN
+            // and fmax / the kEps floor are plain maxima: two v_max_f64 instead of five VALU
+            scale[i] = max_raw(max_abs_raw(y[i], y5[i]), kEps);
+        } else {
+            scale[i] = fmax(fabs(y[i]), fabs(y5[i]));
+            if (scale[i] < kEps) scale[i] = kEps;
+        }
         err[i] = fabs(y5[i] - y4);
     }
     // a zero error passes the fast form's per-component test for any positive normal tol, so
