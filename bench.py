@@ -333,7 +333,8 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
         if L.bhrt_frame_wait(t) != 0:
             raise RuntimeError(lib.last_error())
 
-    sync_frame()
+    for _ in range(depth):  # the library's three frame slots each allocate their pinned
+        sync_frame()         # staging on first use: steady state, as in a render loop
     t0 = time.perf_counter()
     for _ in range(frames):
         sync_frame()
