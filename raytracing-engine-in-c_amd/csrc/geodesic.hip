@@ -1423,9 +1423,12 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, 256, 0, st>>>(kp);
-    // rays evicted by the large-argument check (normally none: every wave exits at once)
-    k_trace<METHOD, DISK, SPIN0, FAR, true, INL><<<blocks < cap_huge ? blocks : cap_huge, 256, 0,
-                                                   st>>>(kp);
+    // rays evicted by the large-argument check (normally none: every wave exits at once). 64
+    // workgroups: the evicted rays are rare, and a full-chip grid of waves that only read the
+    // count and exit costs ~15 us per frame (C3 +8.5% same-box, profiles/r02_ab_v24.txt)
+    const int redo_blocks = blocks < 64 ? blocks : 64;
+    k_trace<METHOD, DISK, SPIN0, FAR, true, INL>
+        <<<redo_blocks < cap_huge ? redo_blocks : cap_huge, 256, 0, st>>>(kp);
 }
 
 template <int METHOD, bool DISK, bool SPIN0, bool FAR>
