@@ -1259,7 +1259,10 @@ __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
             const double rxy = sqrt(hx * hx + hy * hy);  // raytracer.c:201-228
             double nr = (rxy - sc.disk_in) / (sc.disk_out - sc.disk_in);
             nr = clampd(nr, 0.0, 1.0);
-            const double T = clampd(sc.disk_tscale * (2000.0 + 18000.0 * pow(1.0 - nr, 0.75)),
+            // pow(1 - nr, 0.75) as sqrt(u) * sqrt(sqrt(u)), u in [0, 1] (a few ulp: the colour
+            // contract's tolerance is 1e-5)
+            const double su = sqrt(1.0 - nr);
+            const double T = clampd(sc.disk_tscale * (2000.0 + 18000.0 * (su * sqrt(su))),
                                     1000.0, 40000.0);  // math_util.c:463-503
             const double t = (T - 1000.0) / (40000.0 - 1000.0);
             r = (t < 0.5) ? t * 2.0 : 1.0;
@@ -1270,10 +1273,19 @@ __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
             g *= br;
             b *= br;
             if (sc.flags & BHRT_FLAG_DOPPLER) {  // raytracer.c:233-294
+                // sin, cos of atan2(hy, hx) as hy / rxy, hx / rxy (rxy > 0: a disk hit lies at
+                // rxy >= disk_in), pow(dop, 4) as two squarings, dop / (1 / sqrt(f)) as
+                // dop * sqrt(f): each within a few ulp of the libm forms
                 double sp, cp;
-                sincos(atan2(hy, hx), &sp, &cp);
+                if (rxy > 0.0) {
+                    const double ir = 1.0 / rxy;
+                    sp = hy * ir;
+                    cp = hx * ir;
+                } else {
+                    sincos(atan2(hy, hx), &sp, &cp);
+                }
                 const double dop = 1.0 + ((dx * -sp + dy * cp) + dz * 0.0) * 0.5;
-                const double z = dop / (1.0 / sqrt(1.0 - sc.rs / rxy));
+                const double z = dop * sqrt(1.0 - sc.rs / rxy);
                 if (z < 1.0) {
                     b *= z;
                     r = fmin(1.0, r * (2.0 - z));
@@ -1281,7 +1293,7 @@ __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
                     r *= 2.0 - z;
                     b = fmin(1.0, b * z);
                 }
-                const double beam = pow(dop, 4.0);
+                const double d2 = dop * dop, beam = d2 * d2;
                 r = clampd(r * beam, 0.0, 1.0);
                 g = clampd(g * beam, 0.0, 1.0);
                 b = clampd(b * beam, 0.0, 1.0);
