@@ -442,6 +442,8 @@ static void fill_camera(bhrt_kparams* kp, const bhrt_camera* cam, int W, int H) 
     k->off_y = cam->use_offset ? cam->offset_y : 0.5;
     k->width = W;
     k->height = H;
+    k->inv_width = 1.0 / (double)W;
+    k->inv_block = 1.0 / (double)k->rows.row_block;
     k->pos[0] = cam->position.x;
     k->pos[1] = cam->position.y;
     k->pos[2] = cam->position.z;
@@ -572,7 +574,10 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
     bhrt_kparams kp;
     fill_scene(&kp, bh, dk, cfg, method, flags);
     fill_camera(&kp, cam, W, H);
-    if (rows && rows->num_shards > 1) kp.cam.rows = *rows;
+    if (rows && rows->num_shards > 1) {
+        kp.cam.rows = *rows;
+        kp.cam.inv_block = 1.0 / (double)rows->row_block;
+    }
     kp.n = nrows * W;
     kp.init = (double*)scratch;
     kp.out = *out;

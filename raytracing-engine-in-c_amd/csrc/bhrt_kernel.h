@@ -46,6 +46,7 @@ typedef struct {
     double off_x, off_y;             /* sub-pixel offset (0.5, 0.5 = centre)   */
     int width, height;
     bhrt_rows rows;
+    double inv_width, inv_block;     /* RN(1 / width), RN(1 / rows.row_block)  */
     /* shared origin (integrate_photon_path set-up, raytracer.c:355-466) */
     double pos[3];                   /* Cartesian origin                        */
     double r0, th0, ph0;             /* cartesian_to_spherical(origin)          */

@@ -702,15 +702,26 @@ __device__ __forceinline__ void ray_init_general(Ray_& R, double t0, double ox, 
     R.k = 0;
 }
 
+// floor(a / d) for 0 <= a < 2^31, d >= 1, from inv = RN(1 / d): RN(a * inv) is within 2^-52
+// relative of a / d, so its truncation is the quotient or one below it (never above: a / d
+// ends at least 1 / d short of the next integer, and d (q + 1) < 2^52), and one test fixes it
+// -- a few VALU instead of the ~30 of a 32-bit integer division
+__device__ __forceinline__ int div_floor(int a, int d, double inv) {
+    int q = (int)((double)a * inv);
+    if ((unsigned)(q + 1) * (unsigned)d <= (unsigned)a) q++;
+    return q;
+}
+
 // calculate_ray_direction (raytracer.c:1013-1038) for pixel-centre ray i of the shard
 __device__ __forceinline__ void camera_dir(const bhrt_camera_k& cm, int i, double& dx,
                                            double& dy, double& dz) {
     const int W = cm.width;
-    const int j = i / W, px = i - j * W;
+    const int j = div_floor(i, W, cm.inv_width), px = i - j * W;
     int py = j;
     if (cm.rows.num_shards > 1) {
         const int B = cm.rows.row_block;
-        py = ((j / B) * cm.rows.num_shards + cm.rows.shard) * B + j % B;
+        const int jb = div_floor(j, B, cm.inv_block);
+        py = (jb * cm.rows.num_shards + cm.rows.shard) * B + (j - jb * B);
     }
     const double ndcx = (2.0 * ((px + cm.off_x) / W) - 1.0) * cm.plane_w;
     const double ndcy = (1.0 - 2.0 * ((py + cm.off_y) / cm.height)) * cm.plane_h;
