@@ -45,6 +45,41 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _launch_ranks():
+    """`python bench.py --gpus N` (N > 1) with no launcher around it: start the N rank
+    processes here, one per GPU, through torch.distributed.run (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set for every child), and exit with the
+    launcher's exit code (the worst rank's). Rank 0's JSON line reaches stdout through the
+    inherited descriptor. This runs BEFORE torch or libbhrt is imported: the parent never
+    touches a GPU, so no process that initialised HIP ever starts another program. Returns
+    only when no launch is needed (N = 1, or a launcher already set WORLD_SIZE)."""
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument("--gpus", type=int, default=1)
+    n = p.parse_known_args()[0].gpus
+    if n <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    rc = subprocess.call(cmd, env=dict(os.environ))
+    if os.environ.get("BHRT_BENCH_DRYRUN"):  # tests: did this process ever load HIP?
+        with open("/proc/self/maps") as f:
+            hip = "libamdhip64" in f.read()
+        print(json.dumps({"launcher": True, "rc": rc, "hip_loaded": hip,
+                          "torch_imported": "torch" in sys.modules}), flush=True)
+    sys.exit(rc)
+
+
+if __name__ == "__main__":
+    _launch_ranks()
+
 sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
 
 import numpy as np  # noqa: E402
@@ -52,8 +87,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from bhrt import abi, configs, lib  # noqa: E402
-from bhrt.dist_frame import (FramePipeline, padded_shard_rows, sample_offset,  # noqa: E402
-                             shard_row_count)
+from bhrt.dist_frame import (DISPLAY_FIELD, RGB_FIELDS, FramePipeline,  # noqa: E402
+                             padded_shard_rows, sample_offset, shard_row_count)
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (and FP64 matrix) peak, AMD spec
 METRIC = "Mrays/s (and RK4 steps/s) per GPU + per node; max |Δhit| vs CPU ref"
@@ -91,9 +126,11 @@ def parse():
     p.add_argument("--shard", type=int, default=None,
                    help="tiles mode, N = 1: render shard K of the frame instead of shard 0 "
                         "(to time every shard of a node frame on one GPU)")
-    p.add_argument("--gather", choices=("image", "all"), default="image",
-                   help="fields gathered to rank 0: the colour planes (24 B/ray, default) or "
-                        "every SoA field (96 B/ray)")
+    p.add_argument("--gather", choices=("rgba8", "image", "all"), default="rgba8",
+                   help="fields gathered to rank 0 at N > 1: the rgba8 display buffer the "
+                        "colour pass writes (4 B/ray, default), the f64 colour planes "
+                        "(24 B/ray) or every SoA field (96 B/ray); every rank keeps its "
+                        "shard's full f64 SoA resident either way")
     return p.parse_args()
 
 
@@ -132,10 +169,23 @@ def main():
         raise SystemExit("--streams must be 1 or 2")
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # rehearsal of the N-GPU path on a one-GPU box: every rank on GPU 0, gloo collectives
+    # (RCCL refuses two ranks on one device); the product N-GPU run never sets this
+    shared = os.environ.get("BHRT_BENCH_SHARE_DEVICE") == "1"
+    if os.environ.get("BHRT_BENCH_DRYRUN"):  # tests: the rank environment, no GPU call
+        print(json.dumps({"rank": rank, "local_rank": local, "world_size": world,
+                          "master_addr": os.environ.get("MASTER_ADDR"),
+                          "master_port": os.environ.get("MASTER_PORT"),
+                          "device": 0 if shared else local}), flush=True)
+        return
+    dev_index = 0 if shared else local
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
     L = lib.load()
     if args.refill:
         L.bhrt_set_refill_threshold(args.refill)
@@ -161,9 +211,12 @@ def main():
         rays_frame = sum(shard_row_count(H, B, r, S) for r in range(world)) * W
         if args.shard is not None and world == 1:
             rays_frame = shard_row_count(H, B, shard, S) * W
-    gather = None if args.gather == "all" else dist_frame_rgb()
+    if samples and args.gather == "rgba8":
+        args.gather = "image"  # (samples mode averages the f64 colour planes)
+    gather = {"all": None, "image": RGB_FIELDS, "rgba8": DISPLAY_FIELD}[args.gather]
+    fields = FIELDS + DISPLAY_FIELD if args.gather == "rgba8" else FIELDS
     pipe = FramePipeline(n, device, world, rank, "samples" if samples else "shards", H, W, B,
-                         FIELDS, shards=S, gather=gather, first_shard=shard - rank)
+                         fields, shards=S, gather=gather, first_shard=shard - rank)
     streams = ([torch.cuda.current_stream()] if args.streams <= 1 else
                [torch.cuda.Stream(device) for _ in range(args.streams)])
     frame_no = [0]
@@ -199,10 +252,11 @@ def main():
     elapsed = time.perf_counter() - t0
     st = lib.stats(reset=True)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        red = "cpu" if shared else device  # (gloo reduces host tensors)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-        tot = torch.tensor([st["iterations"]], dtype=torch.float64, device=device)
+        tot = torch.tensor([st["iterations"]], dtype=torch.float64, device=red)
         dist.all_reduce(tot)
         iterations_all = tot.item()
     else:
@@ -382,11 +436,6 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
                     "in flight; trace_rays_batch = the reference batch API on the frame's camera "
                     "rays (RayTraceHit[] out); trace_ray = median of one drop-in call, PCIe "
                     "round trip included"}
-
-
-def dist_frame_rgb():
-    from bhrt.dist_frame import RGB_FIELDS
-    return RGB_FIELDS
 
 
 def pmc_profile(config):

@@ -94,6 +94,20 @@ DISPLAY_FIELDS = ("rgba32f", "rgba8")
 SOA_DTYPES.update(rgba32f=np.float32, rgba8=np.uint8)
 
 
+def rgba8_from_rgb(r, g, b):
+    """The display conversion of bhrt_frame_soa.rgba8 in numpy (renderer.cpp:2090-2125):
+    (unsigned char)(std::min(1.0f, (float)v) * 255.0f) per channel (NaN -> 255, truncation),
+    alpha 255. Returns uint8 [n, 4]."""
+    out = np.empty(np.shape(r) + (4,), dtype=np.uint8)
+    for i, v in enumerate((r, g, b)):
+        f = np.asarray(v).astype(np.float32)
+        with np.errstate(invalid="ignore"):
+            m = np.where(f < np.float32(1.0), f, np.float32(1.0))
+        out[..., i] = (m * np.float32(255.0)).astype(np.uint8)
+    out[..., 3] = 255
+    return out
+
+
 class FrameSoA(C.Structure):
     _fields_ = [(f, C.c_void_p) for f in SOA_FIELDS + DISPLAY_FIELDS]
 

@@ -33,6 +33,19 @@ from . import abi
 
 INT_FIELDS = ("result", "steps")
 RGB_FIELDS = ("rgb_r", "rgb_g", "rgb_b")
+DISPLAY_FIELD = ("rgba8",)  # the display buffer (4 B per pixel): bench.py's default gather
+# per-ray layout of a field in the FrameBuffer: (element dtype, elements per ray)
+_LAYOUT = {"result": (torch.int32, 1), "steps": (torch.int32, 1),
+           "rgba8": (torch.uint8, 4), "rgba32f": (torch.float32, 4)}
+
+
+def field_layout(f):
+    return _LAYOUT.get(f, (torch.float64, 1))
+
+
+def field_bytes(f):
+    dt, k = field_layout(f)
+    return k * torch.empty(0, dtype=dt).element_size()
 
 
 def shard_row_count(H, row_block, shard, num_shards):
@@ -64,18 +77,19 @@ def shard_rows_index(H, row_block, shard, num_shards):
 
 
 class FrameBuffer:
-    """All SoA fields of n rays carved from one uint8 tensor (8-byte aligned views): the
-    int32 fields first, then the doubles in the order given (abi.SOA_FIELDS ends with the
-    colour planes, so they form the buffer's contiguous tail)."""
+    """All SoA fields of n rays carved from one uint8 tensor (aligned views): the 4-byte
+    fields first (int32 result/steps, the rgba8 display buffer), then the doubles in the order
+    given (abi.SOA_FIELDS ends with the colour planes, so they form a contiguous range), then
+    the 16-byte rgba32f buffer if requested."""
 
     def __init__(self, n, device, fields=abi.SOA_FIELDS):
         self.n = n
         self.fields = tuple(fields)
-        sizes = {f: (4 if f in INT_FIELDS else 8) for f in self.fields}
+        sizes = {f: field_bytes(f) for f in self.fields}
         self.offsets, o = {}, 0
-        for f in sorted(self.fields, key=lambda f: sizes[f]):  # int32 fields first (stable)
-            if sizes[f] == 8:
-                o = (o + 7) // 8 * 8                          # then 8-byte aligned doubles
+        for f in sorted(self.fields, key=lambda f: sizes[f]):  # 4-byte fields first (stable)
+            if sizes[f] >= 8:
+                o = (o + 15) // 16 * 16 if sizes[f] > 8 else (o + 7) // 8 * 8
             self.offsets[f] = (o, o + sizes[f] * n)
             o += sizes[f] * n
         self.nbytes = o
@@ -84,7 +98,9 @@ class FrameBuffer:
 
     def view(self, buf, f):
         a, b = self.offsets[f]
-        return buf[a:b].view(torch.int32 if f in INT_FIELDS else torch.float64)
+        dt, k = field_layout(f)
+        v = buf[a:b].view(dt)
+        return v.view(-1, k) if k > 1 else v
 
     def span(self, fields):
         """(first, last) byte of `fields`, which must be one contiguous range of the buffer."""
@@ -154,6 +170,7 @@ class FramePipeline:
         self.frames = 0
         self.last = None
         self.images = self.gathered = self.colour = None
+        self.staged = False
         if mode == "samples":
             if world > 1:  # per slot: the colour planes summed over ranks (in place on rank 0)
                 self.colour = [torch.empty(len(self.gather), n, dtype=torch.float64,
@@ -166,8 +183,19 @@ class FramePipeline:
             self.gathered = [torch.empty(world, b - a, dtype=torch.uint8, device=device)
                              for _ in range(2)]
             rows = padded_shard_rows(H, row_block, self.shards) * self.shards
-            self.images = [{f: torch.zeros(rows, W, dtype=fb.views[f].dtype, device=device)
+            self.images = [{f: torch.zeros(rows, W, *self._inner(f), dtype=fb.views[f].dtype,
+                                        device=device)
                             for f in self.gather} for _ in range(2)]
+        # gloo gathers host tensors only: with device buffers (the one-GPU rehearsal of the
+        # N-rank bench, BHRT_BENCH_SHARE_DEVICE) the gathered range travels through host
+        # copies; RCCL gathers the device buffers directly
+        self.staged = (world > 1 and torch.device(device).type != "cpu" and
+                       dist.get_backend() == "gloo")
+        if self.staged:
+            a, b = self.span
+            self.host_send = [torch.empty(b - a, dtype=torch.uint8) for _ in range(2)]
+            self.host_recv = ([torch.empty(world, b - a, dtype=torch.uint8) for _ in range(2)]
+                              if rank == 0 else None)
 
     def next_buffer(self):
         slot = self.frames % 2
@@ -186,6 +214,10 @@ class FramePipeline:
                 self.works[slot] = dist.reduce(col, dst=0, op=dist.ReduceOp.SUM, async_op=True)
             else:
                 self.works[slot] = True
+        elif self.world > 1 and self.staged:
+            self.host_send[slot].copy_(fb.buf[a:b])  # (waits for the render on this stream)
+            recv = list(self.host_recv[slot].unbind(0)) if self.rank == 0 else None
+            self.works[slot] = dist.gather(self.host_send[slot], recv, dst=0, async_op=True)
         elif self.world > 1:
             recv = list(self.gathered[slot].unbind(0)) if self.rank == 0 else None
             self.works[slot] = dist.gather(fb.buf[a:b], recv, dst=0, async_op=True)
@@ -206,17 +238,25 @@ class FramePipeline:
             return
         if w is not True:
             w.wait()
+            if self.staged and self.rank == 0:
+                self.gathered[slot].copy_(self.host_recv[slot])
         self.works[slot] = None
         if self.rank == 0:
             self.last = self._assemble(slot)
 
     def _local(self, fb):
         if self.mode == "samples":
-            return ({f: fb.views[f].view(self.H, self.W) for f in fb.fields},
+            return ({f: fb.views[f].view(self.H, self.W, *self._inner(f)) for f in fb.fields},
                     np.arange(self.H))
         idx = shard_rows_index(self.H, self.row_block, self.first, self.shards)
         rows = fb.n // self.W
-        return {f: fb.views[f].view(rows, self.W)[:len(idx)] for f in fb.fields}, idx
+        return {f: fb.views[f].view(rows, self.W, *self._inner(f))[:len(idx)]
+                for f in fb.fields}, idx
+
+    @staticmethod
+    def _inner(f):
+        k = field_layout(f)[1]
+        return (k,) if k > 1 else ()
 
     def _assemble(self, slot):
         fb, H, W, world = self.bufs[slot], self.H, self.W, self.world
@@ -237,9 +277,11 @@ class FramePipeline:
         image = {}
         for f in self.gather:
             a, b = fb.offsets[f]
-            src = src_all[:, a - a0:b - a0].view(fb.views[f].dtype).view(world, nbk, B, W)
+            inner = self._inner(f)
+            src = src_all[:, a - a0:b - a0].view(fb.views[f].dtype).view(world, nbk, B, W,
+                                                                          *inner)
             dst = self.images[slot][f]
-            dst.view(nbk, S, B, W)[:, self.first:self.first + world].copy_(
-                src.permute(1, 0, 2, 3))
+            dst.view(nbk, S, B, W, *inner)[:, self.first:self.first + world].copy_(
+                src.transpose(0, 1))
             image[f] = dst[:H]
         return Assembled(image, local, idx)

@@ -764,11 +764,23 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
  * finished chunk is copied on the copy stream into pinned staging while later chunks trace,
  * and un-permuted into the caller's arrays by OpenMP threads when the frame is waited for
  * (the next frames in flight keep the GPU busy meanwhile). Opt-in (BHRT_HOST_REGISTER=1): the
- * caller's arrays are page-locked while the GPU traces (hipHostRegister) and each chunk is
- * DMA'd straight into them, one 2-D copy per field un-permuting the row blocks.
- * DESIGN.md §4 "Host-buffer frames". */
+ * whole pages INSIDE each of the caller's arrays are page-locked while the GPU traces
+ * (hipHostRegister) and each chunk is DMA'd straight into them, one 2-D copy per field
+ * un-permuting the row blocks; the bytes of an array's partial first and last pages go
+ * through staging. DESIGN.md §4 "Host-buffer frames". */
+#define BHRT_EDGE_STAGE ((size_t)BHRT_NFIELDS * 2 * 4096)
+
 typedef struct {
-    int active, ticket, ndev, K, shards, W, H, direct, nreg;
+    size_t stage_off; /* in the device's pinned staging of the frame slot */
+    char* dst;        /* caller memory */
+    size_t bytes;
+    int dev;
+} edge_piece;
+
+typedef struct {
+    int active, ticket, ndev, K, shards, W, H, direct;
+    int reaped_ticket, reaped_rc; /* a frame a later issue waited for implicitly */
+    unsigned long long last_use;
     int timing;             /* BHRT_HOST_TIMING: print where the frame's time went (device 0) */
     hipEvent_t t_ev[2 + 2 * BHRT_MAX_CHUNKS];
     double t_host[4];
@@ -776,79 +788,123 @@ typedef struct {
     shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
     bhrt_rows rows[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
     size_t stage_off[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
-    void* reg[BHRT_NFIELDS]; /* page ranges this frame registered (unregistered at wait) */
+    /* direct mode: [rlo, rhi) = the registered whole pages inside field f's array (0 = none) */
+    uintptr_t rlo[BHRT_NFIELDS], rhi[BHRT_NFIELDS];
+    edge_piece* pieces;     /* staged bytes outside [rlo, rhi), copied into place at wait */
+    int npieces, cap_pieces;
+    size_t edge_stage[BHRT_MAX_DEV];
 } host_frame;
 
 static _Thread_local host_frame* g_frames; /* [BHRT_FRAME_SLOTS], allocated on first use */
 static _Thread_local int g_next_ticket;
+static _Thread_local unsigned long long g_frame_clock;
 
 static void unregister_host(host_frame* f) {
-    for (int i = 0; i < f->nreg; i++) (void)hipHostUnregister(f->reg[i]);
-    f->nreg = 0;
+    for (int k = 0; k < BHRT_NFIELDS; k++)
+        if (f->rlo[k]) {
+            (void)hipHostUnregister((void*)f->rlo[k]);
+            f->rlo[k] = f->rhi[k] = 0;
+        }
 }
 
-/* Register the pages of every field the caller asked for (merged into disjoint ranges). Pages
- * the caller registered itself are used as they are. Returns 0 when every field is DMA-able. */
+/* Page-lock the whole pages inside each requested field's array: [round up(p), round down(p +
+ * bytes)). Nothing outside the caller's arrays is ever registered, so no other allocation
+ * can start inside a registered page (see DESIGN.md §4 for why that matters), and arrays of
+ * different frames never share a registration. Any failure -- a range the caller (or anyone
+ * else) registered already, an array shorter than two pages -- unregisters what this frame
+ * registered and returns -1: the frame then stages. */
 static int register_host(host_frame* f) {
     const uintptr_t pg = 4096;
-    uintptr_t a[BHRT_NFIELDS], b[BHRT_NFIELDS];
-    int n = 0;
     for (int k = 0; k < BHRT_NFIELDS; k++) {
+        f->rlo[k] = f->rhi[k] = 0;
         const uintptr_t p = (uintptr_t)*soa_slot(&f->host, k);
         if (!p) continue;
-        const uintptr_t lo = p & ~(pg - 1),
-                        hi = (p + k_fsize[k] * (size_t)f->W * (size_t)f->H + pg - 1) & ~(pg - 1);
-        int i = n++; /* insertion sort by start */
-        while (i > 0 && a[i - 1] > lo) {
-            a[i] = a[i - 1];
-            b[i] = b[i - 1];
-            i--;
-        }
-        a[i] = lo;
-        b[i] = hi;
-    }
-    f->nreg = 0;
-    for (int i = 0; i < n;) {
-        uintptr_t lo = a[i], hi = b[i];
-        for (i++; i < n && a[i] <= hi; i++)
-            if (b[i] > hi) hi = b[i];
-        const hipError_t e = hipHostRegister((void*)lo, hi - lo, hipHostRegisterPortable);
-        if (e == hipSuccess) {
-            f->reg[f->nreg++] = (void*)lo;
-        } else {
+        const uintptr_t lo = (p + pg - 1) & ~(pg - 1),
+                        hi = (p + k_fsize[k] * (size_t)f->W * (size_t)f->H) & ~(pg - 1);
+        if (hi < lo + 2 * pg || hipHostRegister((void*)lo, hi - lo, hipHostRegisterPortable) !=
+                                    hipSuccess) {
             (void)hipGetLastError();
-            if (e != hipErrorHostMemoryAlreadyRegistered) {
-                unregister_host(f);
-                return -1;
-            }
+            unregister_host(f);
+            return -1;
         }
+        f->rlo[k] = lo;
+        f->rhi[k] = hi;
     }
     return 0;
 }
 
-/* DMA a finished chunk's wanted fields straight into the (registered) caller arrays: local
- * row block i of shard sh is image block i*S + sh, so the full blocks are one 2-D copy per
- * field and a partial last block one more copy. */
-static int copy_chunk_direct(const shard_job* j, const bhrt_frame_soa* host, int W,
-                             const bhrt_rows* rows, hipStream_t st) {
-    for (int f = 0; f < BHRT_NFIELDS; f++) {
-        if (!WANTED(j, host, f)) continue;
-        char* dst = (char*)*soa_slot((bhrt_frame_soa*)host, f);
-        const char* src = (const char*)*soa_slot((bhrt_frame_soa*)&j->dev, f);
-        const size_t fs = k_fsize[f];
+static int add_piece(host_frame* f, int dev, size_t stage_off, char* dst, size_t bytes) {
+    if (f->npieces == f->cap_pieces) {
+        const int cap = f->cap_pieces ? 2 * f->cap_pieces : 64;
+        edge_piece* p = (edge_piece*)realloc(f->pieces, (size_t)cap * sizeof *p);
+        if (!p) {
+            set_err("host allocation failed");
+            return -1;
+        }
+        f->pieces = p;
+        f->cap_pieces = cap;
+    }
+    f->pieces[f->npieces++] = (edge_piece){stage_off, dst, bytes, dev};
+    return 0;
+}
+
+/* D2H of the device bytes [src, src + n) that land at caller address dst: the part inside
+ * the field's registered pages [rlo, rhi) by DMA, the parts outside (an array's partial first
+ * and last pages) into the device's edge staging, placed at wait */
+static int copy_span(host_frame* f, int dev, int fld, char* dst, const char* src, size_t n,
+                     char* stage, hipStream_t st) {
+    const uintptr_t a = (uintptr_t)dst, b = a + n, lo = f->rlo[fld], hi = f->rhi[fld];
+    const uintptr_t ia = a > lo ? a : lo, ib = b < hi ? b : hi;
+    if (ia < ib)
+        HIP_TRY(hipMemcpyAsync((char*)ia, src + (ia - a), ib - ia, hipMemcpyDeviceToHost, st));
+    const uintptr_t out[2][2] = {{a, b < lo ? b : lo}, {a > hi ? a : hi, b}};
+    for (int i = 0; i < 2; i++) {
+        if (out[i][0] >= out[i][1]) continue;
+        const size_t m = out[i][1] - out[i][0], off = f->edge_stage[dev];
+        if (off + m > BHRT_EDGE_STAGE) { /* (cannot happen: < 2 pages per field) */
+            set_err("edge staging overflow");
+            return -1;
+        }
+        f->edge_stage[dev] += m;
+        HIP_TRY(hipMemcpyAsync(stage + off, src + (out[i][0] - a), m, hipMemcpyDeviceToHost, st));
+        if (add_piece(f, dev, off, (char*)out[i][0], m)) return -1;
+    }
+    return 0;
+}
+
+/* DMA a finished chunk's wanted fields into the caller arrays: local row block i of shard sh
+ * is image block i*S + sh, so the blocks inside the registered pages are ONE 2-D copy per
+ * field; the (at most few) blocks that reach into an array's partial first or last page, and a
+ * partial last block, go through copy_span. */
+static int copy_chunk_direct(host_frame* f, int dev, const shard_job* j, const bhrt_rows* rows,
+                             char* stage, hipStream_t st) {
+    const int W = f->W;
+    for (int fld = 0; fld < BHRT_NFIELDS; fld++) {
+        if (!WANTED(j, &f->host, fld)) continue;
+        char* dst = (char*)*soa_slot(&f->host, fld);
+        const char* src = (const char*)*soa_slot((bhrt_frame_soa*)&j->dev, fld);
+        const size_t fs = k_fsize[fld];
         if (!rows || rows->num_shards <= 1) {
-            HIP_TRY(hipMemcpyAsync(dst, src, fs * (size_t)j->n, hipMemcpyDeviceToHost, st));
+            if (copy_span(f, dev, fld, dst, src, fs * (size_t)j->n, stage, st)) return -1;
             continue;
         }
         const size_t rowb = fs * (size_t)W, B = rows->row_block, S = rows->num_shards,
-                     sh = rows->shard;
+                     sh = rows->shard, blk = B * rowb;
         const size_t nrow = (size_t)j->n / W, nfull = nrow / B, rem = nrow % B;
-        if (nfull)
-            HIP_TRY(hipMemcpy2DAsync(dst + sh * B * rowb, S * B * rowb, src, B * rowb, B * rowb,
-                                     nfull, hipMemcpyDeviceToHost, st));
-        if (rem)
-            HIP_TRY(hipMemcpyAsync(dst + (nfull * S + sh) * B * rowb, src + nfull * B * rowb,
-                                   rem * rowb, hipMemcpyDeviceToHost, st));
+        /* full blocks whose destination lies inside [rlo, rhi): a contiguous run [i0, i1) */
+        size_t i0 = 0, i1;
+        while (i0 < nfull && (uintptr_t)(dst + (i0 * S + sh) * blk) < f->rlo[fld]) i0++;
+        i1 = i0;
+        while (i1 < nfull && (uintptr_t)(dst + (i1 * S + sh) * blk) + blk <= f->rhi[fld]) i1++;
+        if (i1 > i0)
+            HIP_TRY(hipMemcpy2DAsync(dst + (i0 * S + sh) * blk, S * blk, src + i0 * blk, blk, blk,
+                                     i1 - i0, hipMemcpyDeviceToHost, st));
+        for (size_t i = 0; i < nfull + (rem ? 1 : 0); i++) {
+            if (i >= i0 && i < i1) continue;
+            const size_t bytes = i < nfull ? blk : rem * rowb;
+            if (copy_span(f, dev, fld, dst + (i * S + sh) * blk, src + i * blk, bytes, stage, st))
+                return -1;
+        }
     }
     return 0;
 }
@@ -867,26 +923,17 @@ static int frame_chunks(int ndev, int W, int H, int block) {
     return K;
 }
 
-int bhrt_frame_wait(int ticket) {
-    if (!g_frames || ticket <= 0) {
-        set_err("no such frame ticket %d", ticket);
-        return -1;
-    }
-    host_frame* f = &g_frames[ticket % BHRT_FRAME_SLOTS];
-    if (!f->active || f->ticket != ticket) {
-        set_err("frame ticket %d is not in flight", ticket);
-        return -1;
-    }
-    f->active = 0;
+/* wait for every copy a frame queued, then place its staged bytes and drop its page locks */
+static int frame_complete(host_frame* f) {
+    const int slot = (int)(f - g_frames);
     int rc = 0;
     struct timespec tw0;
     clock_gettime(CLOCK_MONOTONIC, &tw0);
     for (int k = 0; k < f->K && rc == 0; k++)
         for (int d = 0; d < f->ndev && rc == 0; d++) {
             devctx_t* c = f->jobs[k][d].c;
-            const int slot = ticket % BHRT_FRAME_SLOTS;
             if (hipSetDevice(d) != hipSuccess || hipEventSynchronize(c->fr[slot].copied[k]) != hipSuccess) {
-                set_err("frame %d: waiting for chunk %d of device %d failed", ticket, k, d);
+                set_err("frame %d: waiting for chunk %d of device %d failed", f->ticket, k, d);
                 rc = -1;
                 break;
             }
@@ -894,6 +941,12 @@ int bhrt_frame_wait(int ticket) {
                 readback_finish(&f->jobs[k][d], &f->host,
                                 (const char*)c->fr[slot].h_stage + f->stage_off[k][d], f->W,
                                 f->shards > 1 ? &f->rows[k][d] : NULL);
+        }
+    if (rc == 0 && f->direct)
+        for (int i = 0; i < f->npieces; i++) {
+            const edge_piece* p = &f->pieces[i];
+            memcpy(p->dst, (const char*)f->jobs[0][p->dev].c->fr[slot].h_stage + p->stage_off,
+                   p->bytes);
         }
     unregister_host(f);
     if (f->timing && rc == 0) {
@@ -905,7 +958,7 @@ int bhrt_frame_wait(int ticket) {
             (void)hipEventElapsedTime(&cp[k], f->t_ev[0], f->t_ev[3 + 2 * k]);
         }
         fprintf(stderr, "libbhrt frame %d (%s, K=%d): enqueue %.2f ms, register %.2f ms, copies "
-                "queued %.2f ms, wait %.2f ms |", ticket, f->direct ? "direct" : "staging", f->K,
+                "queued %.2f ms, wait %.2f ms |", f->ticket, f->direct ? "direct" : "staging", f->K,
                 f->t_host[0], f->t_host[1], f->t_host[2],
                 (tw1.tv_sec - tw0.tv_sec) * 1e3 + (tw1.tv_nsec - tw0.tv_nsec) * 1e-6);
         for (int k = 0; k < f->K; k++) fprintf(stderr, " chunk %d traced %.2f copied %.2f", k, tr[k], cp[k]);
@@ -914,39 +967,70 @@ int bhrt_frame_wait(int ticket) {
     return rc;
 }
 
-static int render_frame_issue(const BlackHoleParams* bh, const AccretionDiskParams* dk,
-                              const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
-                              IntegrationMethod method, int flags, const bhrt_frame_soa* host,
-                              int* ticket_out) {
-    if (ticket_out) *ticket_out = 0;
-    if (check_scene(bh, cfg) || !cam || !host || W <= 0 || H <= 0) {
-        if (!g_err[0]) set_err("invalid argument");
+int bhrt_frame_wait(int ticket) {
+    if (!g_frames || ticket <= 0) {
+        set_err("no such frame ticket %d", ticket);
         return -1;
     }
-    int ndev = bhrt_device_count();
-    if (ndev <= 0) {
-        set_err("no HIP device available (libbhrt has no CPU path)");
-        return -1;
+    for (int s = 0; s < BHRT_FRAME_SLOTS; s++) {
+        host_frame* f = &g_frames[s];
+        if (f->active && f->ticket == ticket) {
+            f->active = 0;
+            return frame_complete(f);
+        }
+        if (f->reaped_ticket == ticket) { /* completed when a later issue needed its slot */
+            f->reaped_ticket = 0;
+            if (f->reaped_rc) set_err("frame %d failed", ticket);
+            return f->reaped_rc;
+        }
     }
-    if (!g_frames && !(g_frames = (host_frame*)calloc(BHRT_FRAME_SLOTS, sizeof(host_frame)))) {
-        set_err("host allocation failed");
-        return -1;
+    set_err("frame ticket %d is not in flight", ticket);
+    return -1;
+}
+
+/* The slot for a new frame: an idle slot, the most recently used one first (its buffers are
+ * warm: a caller of the synchronous API keeps reusing ONE slot's device SoA and pinned
+ * staging); with every slot in flight, the oldest frame is completed first and its result kept
+ * for its own bhrt_frame_wait. */
+static host_frame* frame_slot(void) {
+    host_frame* best = NULL;
+    for (int s = 0; s < BHRT_FRAME_SLOTS; s++) {
+        host_frame* f = &g_frames[s];
+        if (!f->active && (!best || f->last_use > best->last_use)) best = f;
     }
-    const int ticket = ++g_next_ticket, slot = ticket % BHRT_FRAME_SLOTS;
-    host_frame* f = &g_frames[slot];
-    if (f->active && bhrt_frame_wait(f->ticket)) return -1; /* the slot's previous frame */
-    const int block = 8;
-    if (ndev > 1 && H < ndev * block) ndev = 1;
-    const int K = frame_chunks(ndev, W, H, block), shards = K * ndev;
-    f->ticket = ticket;
-    f->ndev = ndev;
-    f->K = K;
-    f->shards = shards;
-    f->W = W;
-    f->H = H;
-    f->host = *host;
-    f->nreg = 0;
-    f->timing = getenv("BHRT_HOST_TIMING") != NULL;
+    if (best) return best;
+    for (int s = 0; s < BHRT_FRAME_SLOTS; s++)
+        if (!best || g_frames[s].ticket < best->ticket) best = &g_frames[s];
+    best->active = 0;
+    best->reaped_rc = frame_complete(best);
+    best->reaped_ticket = best->ticket;
+    return best;
+}
+
+/* A frame whose issue failed part way: its launches and copies may still be queued on the
+ * slot's buffers and the caller's pages, so drain every stream it used before the page locks
+ * go and the caller sees the error (the caller may then free its arrays). */
+static void frame_abort(host_frame* f, int ndev) {
+    char err[sizeof g_err];
+    memcpy(err, g_err, sizeof err);
+    for (int d = 0; d < ndev; d++) {
+        devctx_t* c = g_ctx[d];
+        if (!c || hipSetDevice(d) != hipSuccess) continue;
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->stream2);
+        (void)hipStreamSynchronize(c->copy);
+    }
+    unregister_host(f);
+    f->active = 0;
+    memcpy(g_err, err, sizeof err);
+}
+
+static int frame_enqueue(host_frame* f, const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                         const SimulationConfig* cfg, const bhrt_camera* cam,
+                         IntegrationMethod method, int flags) {
+    const int slot = (int)(f - g_frames), ticket = f->ticket, ndev = f->ndev, K = f->K,
+              shards = f->shards, W = f->W, H = f->H, block = 8;
+    const bhrt_frame_soa* host = &f->host;
     struct timespec th[4];
     clock_gettime(CLOCK_MONOTONIC, &th[0]);
     if (f->timing && !f->t_ev[0]) {
@@ -994,28 +1078,30 @@ static int render_frame_issue(const BlackHoleParams* bh, const AccretionDiskPara
     /* Opt-in (BHRT_HOST_REGISTER=1): while the GPU traces, page-lock the caller's arrays and
      * DMA straight into them. It saves the last chunk's host copy of a synchronous frame (C2:
      * 11.0-11.7 vs 12.3-12.9 ms) but is slower with frames in flight (10.3 vs 9.8 ms per
-     * frame), and it pins caller pages -- rounded to whole pages, neighbours included -- for
-     * the frame's flight, with the HIP runtime keeping its record of a registered range past
-     * hipHostUnregister (profiles/r02_host_path.txt), so staging is the default. Frames under
-     * 8 MB always stage. */
+     * frame), so staging is the default. Frames under 8 MB always stage. */
     size_t frame_bytes = 0;
     for (int k = 0; k < BHRT_NFIELDS; k++)
-        if (*soa_slot(&f->host, k)) frame_bytes += k_fsize[k] * (size_t)W * (size_t)H;
+        if (*soa_slot((bhrt_frame_soa*)host, k)) frame_bytes += k_fsize[k] * (size_t)W * (size_t)H;
     const char* reg_env = getenv("BHRT_HOST_REGISTER");
     f->direct = frame_bytes >= ((size_t)8 << 20) && reg_env && atoi(reg_env) > 0 &&
                 register_host(f) == 0;
-    if (!f->direct)
-        for (int d = 0; d < ndev; d++) {
-            devctx_t* c = f->jobs[0][d].c;
-            size_t host_bytes = 0;
+    f->npieces = 0;
+    for (int d = 0; d < ndev; d++) {
+        devctx_t* c = f->jobs[0][d].c;
+        size_t host_bytes = 0;
+        if (f->direct) { /* edge staging: the bytes outside [rlo, rhi), < 2 pages per field */
+            host_bytes = BHRT_EDGE_STAGE;
+            f->edge_stage[d] = 0;
+        } else {
             for (int k = 0; k < K; k++) {
                 f->stage_off[k][d] = host_bytes;
                 host_bytes += wanted_bytes(&f->jobs[k][d], host);
             }
-            HIP_TRY(hipSetDevice(d));
-            if (ensure(&c->fr[slot].h_stage, &c->fr[slot].cap_stage, host_bytes ? host_bytes : 64, 1))
-                return -1;
         }
+        HIP_TRY(hipSetDevice(d));
+        if (ensure(&c->fr[slot].h_stage, &c->fr[slot].cap_stage, host_bytes ? host_bytes : 64, 1))
+            return -1;
+    }
     clock_gettime(CLOCK_MONOTONIC, &th[2]);
     for (int k = 0; k < K; k++) /* each chunk's copy queued behind its trace */
         for (int d = 0; d < ndev; d++) {
@@ -1024,21 +1110,59 @@ static int render_frame_issue(const BlackHoleParams* bh, const AccretionDiskPara
             HIP_TRY(hipStreamWaitEvent(c->copy, c->fr[slot].done[k], 0));
             const bhrt_rows* r = shards > 1 ? &f->rows[k][d] : NULL;
             if (f->jobs[k][d].n > 0 &&
-                (f->direct ? copy_chunk_direct(&f->jobs[k][d], host, W, r, c->copy)
+                (f->direct ? copy_chunk_direct(f, d, &f->jobs[k][d], r,
+                                               (char*)c->fr[slot].h_stage, c->copy)
                            : readback_issue(&f->jobs[k][d], host,
                                             (char*)c->fr[slot].h_stage + f->stage_off[k][d],
-                                            c->copy))) {
-                unregister_host(f);
+                                            c->copy)))
                 return -1;
-            }
             HIP_TRY(hipEventRecord(c->fr[slot].copied[k], c->copy));
             if (f->timing && d == 0) HIP_TRY(hipEventRecord(f->t_ev[3 + 2 * k], c->copy));
         }
     clock_gettime(CLOCK_MONOTONIC, &th[3]);
     for (int i = 0; i < 3; i++)
         f->t_host[i] = (th[i + 1].tv_sec - th[i].tv_sec) * 1e3 + (th[i + 1].tv_nsec - th[i].tv_nsec) * 1e-6;
+    return 0;
+}
+
+static int render_frame_issue(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                              const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                              IntegrationMethod method, int flags, const bhrt_frame_soa* host,
+                              int* ticket_out) {
+    if (ticket_out) *ticket_out = 0;
+    if (check_scene(bh, cfg) || !cam || !host || W <= 0 || H <= 0) {
+        if (!g_err[0]) set_err("invalid argument");
+        return -1;
+    }
+    int ndev = bhrt_device_count();
+    if (ndev <= 0) {
+        set_err("no HIP device available (libbhrt has no CPU path)");
+        return -1;
+    }
+    if (!g_frames && !(g_frames = (host_frame*)calloc(BHRT_FRAME_SLOTS, sizeof(host_frame)))) {
+        set_err("host allocation failed");
+        return -1;
+    }
+    host_frame* f = frame_slot();
+    const int block = 8;
+    if (ndev > 1 && H < ndev * block) ndev = 1;
+    const int K = frame_chunks(ndev, W, H, block);
+    f->ticket = ++g_next_ticket;
+    f->last_use = ++g_frame_clock;
+    f->ndev = ndev;
+    f->K = K;
+    f->shards = K * ndev;
+    f->W = W;
+    f->H = H;
+    f->host = *host;
+    f->direct = 0;
+    f->timing = getenv("BHRT_HOST_TIMING") != NULL;
+    if (frame_enqueue(f, bh, dk, cfg, cam, method, flags)) {
+        frame_abort(f, ndev);
+        return -1;
+    }
     f->active = 1;
-    if (ticket_out) *ticket_out = ticket;
+    if (ticket_out) *ticket_out = f->ticket;
     return 0;
 }
 

@@ -76,6 +76,8 @@ typedef struct {
                                   zeroed per launch */
     int queue_bits;       /* 2^queue_bits ray queues (<= BHRT_MAX_QUEUE_BITS)            */
     int queue_stride;     /* u64 words between queue heads (<= BHRT_QUEUE_STRIDE_MAX)     */
+    int claim_shift;      /* set by the launcher per launch: a block claim is the queue's
+                             remainder >> claim_shift, 2^claim_shift >= waves * claim_div / queues */
 } bhrt_kparams;
 
 /* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and

@@ -1069,11 +1069,8 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const unsigned nq = 1u << qbits;
     unsigned long long* const heads = HUGE ? kp.ctl + 7 : kp.qhead;
     const unsigned qstride = HUGE ? 0u : (unsigned)kp.queue_stride;
-    // claim = remainder >> shift, 2^shift >= waves * claim_div / Q (no division in the loop)
-    const unsigned shift =
-        kp.claim_div > 0
-            ? 32u - __builtin_clz((gridDim.x * (blockDim.x >> 6) * kp.claim_div >> qbits) - 1u | 1u)
-            : 0u;
+    // claim = remainder >> shift (no division in the loop; claim_shift from the launcher)
+    const unsigned shift = (unsigned)kp.claim_shift;
     const int wv = threadIdx.x >> 6;
     if (MULTIQ && lane == 0) {
         s_q[wv][0] = 0u;
@@ -1427,6 +1424,17 @@ int grid_for(const void* fn, int n) {
     return blocks < 1 ? 1 : (int)blocks;
 }
 
+// smallest shift with 2^shift >= (waves * claim_div) / 2^queue_bits, at least 1 (a grid of
+// fewer waves than queues claims half a queue's remainder at a time); 0 = exact claims
+int claim_shift(int blocks, int claim_div, int queue_bits) {
+    if (claim_div <= 0) return 0;
+    const unsigned long long wq =
+        ((unsigned long long)blocks * (256 / 64) * (unsigned)claim_div) >> queue_bits;
+    int shift = 1;
+    while (shift < 31 && (1ull << shift) < wq) shift++;
+    return shift;
+}
+
 template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool INL>
 void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     // resident workgroups of the two instantiations, per device
@@ -1445,13 +1453,16 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     int blocks = (kp.n + 255) / 256;
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
-    k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, 256, 0, st>>>(kp);
+    bhrt_kparams k = kp;
+    k.claim_shift = claim_shift(blocks, kp.claim_div, kp.queue_bits);
+    k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, 256, 0, st>>>(k);
     // rays evicted by the large-argument check (normally none: every wave exits at once). 64
     // workgroups: the evicted rays are rare, and a full-chip grid of waves that only read the
     // count and exit costs ~15 us per frame (C3 +8.5% same-box, profiles/r02_ab_v24.txt)
-    const int redo_blocks = blocks < 64 ? blocks : 64;
-    k_trace<METHOD, DISK, SPIN0, FAR, true, INL>
-        <<<redo_blocks < cap_huge ? redo_blocks : cap_huge, 256, 0, st>>>(kp);
+    int redo_blocks = blocks < 64 ? blocks : 64;
+    if (redo_blocks > cap_huge) redo_blocks = cap_huge;
+    k.claim_shift = claim_shift(redo_blocks, kp.claim_div, 0);  // (the redo list is one queue)
+    k_trace<METHOD, DISK, SPIN0, FAR, true, INL><<<redo_blocks, 256, 0, st>>>(k);
 }
 
 template <int METHOD, bool DISK, bool SPIN0, bool FAR>

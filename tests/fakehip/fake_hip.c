@@ -89,6 +89,40 @@ static int overlaps_registration(uintptr_t a, size_t n) {
     return hit;
 }
 
+/* ---- the caller's host arrays (declared by the driver): page locks must stay inside one of
+ * them, and none may be freed while a lock on it is live (a freed-and-reused page that the
+ * runtime still believes registered is how DMA reaches memory nobody pinned) ---- */
+static alloc_t g_host[1024];
+static int g_nhost;
+
+void fakehip_declare_host(const void* p, size_t n) {
+    pthread_mutex_lock(&g_mu);
+    if (g_nhost == (int)(sizeof g_host / sizeof *g_host)) FAIL("host array table full");
+    g_host[g_nhost++] = (alloc_t){(uintptr_t)p, n, -4};
+    pthread_mutex_unlock(&g_mu);
+}
+void fakehip_forget_host(const void* p) {
+    pthread_mutex_lock(&g_mu);
+    for (int i = 0; i < g_nhost; i++)
+        if (g_host[i].base == (uintptr_t)p) {
+            const uintptr_t a = g_host[i].base, b = a + g_host[i].size;
+            for (int k = 0; k < g_nalloc; k++)
+                if (g_alloc[k].dev == -2 && g_alloc[k].base < b && a < g_alloc[k].base + g_alloc[k].size)
+                    FAIL("caller array %p freed while page-locked", p);
+            g_host[i] = g_host[--g_nhost];
+            break;
+        }
+    pthread_mutex_unlock(&g_mu);
+}
+static int inside_caller_array(uintptr_t a, size_t n) {
+    pthread_mutex_lock(&g_mu);
+    int ok = g_nhost == 0; /* (no declarations: not checked) */
+    for (int i = 0; i < g_nhost; i++)
+        if (a >= g_host[i].base && a + n <= g_host[i].base + g_host[i].size) ok = 1;
+    pthread_mutex_unlock(&g_mu);
+    return ok;
+}
+
 int fakehip_kind_of(const void* p, size_t n) { return kind_of(p, n); }
 int fakehip_current_device(void) { return g_dev; }
 
@@ -145,6 +179,8 @@ hipError_t hipHostFree(void* p) {
 hipError_t hipHostRegister(void* p, size_t n, unsigned flags) {
     (void)flags;
     if (((uintptr_t)p & 4095) || (n & 4095)) FAIL("hipHostRegister of an unaligned range");
+    if (!inside_caller_array((uintptr_t)p, n))
+        FAIL("hipHostRegister of [%p, +%zu): pages outside the caller's arrays", p, n);
     if (overlaps_registration((uintptr_t)p, n)) return ret(hipErrorHostMemoryAlreadyRegistered);
     track(p, n, -2);
     return hipSuccess;

@@ -17,8 +17,9 @@ import torch.multiprocessing as mp
 
 from conftest import ROOT
 from bhrt import abi, configs
-from bhrt.dist_frame import (FrameBuffer, FramePipeline, RGB_FIELDS, padded_shard_rows,
-                             sample_offset, shard_row_count, shard_rows_index)
+from bhrt.dist_frame import (DISPLAY_FIELD, FrameBuffer, FramePipeline, RGB_FIELDS,
+                             padded_shard_rows, sample_offset, shard_row_count,
+                             shard_rows_index)
 
 
 def _free_port():
@@ -45,15 +46,21 @@ def _tiles_worker(rank, world, port, W, H, B, S, gather, frames, cfg_name, max_s
         cam = configs.camera("B")
         rows = abi.Rows(B, rank, S) if S > 1 else None
         n = padded_shard_rows(H, B, S) * W
-        pipe = FramePipeline(n, "cpu", world, rank, "shards", H, W, B, shards=S,
-                             gather=None if gather == "all" else RGB_FIELDS)
+        fields = abi.SOA_FIELDS + (DISPLAY_FIELD if gather == "rgba8" else ())
+        pipe = FramePipeline(n, "cpu", world, rank, "shards", H, W, B, fields, shards=S,
+                             gather={"all": None, "image": RGB_FIELDS,
+                                     "rgba8": DISPLAY_FIELD}[gather])
         part = orc.oracle().render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags, rows=rows,
                                          threads=2)
         for i in range(frames):
             fb = pipe.next_buffer()
-            for f in fb.fields:
+            for f in abi.SOA_FIELDS:
                 v = torch.from_numpy(part[f])
                 fb.views[f][:len(v)].copy_(v * (i + 1) if f in RGB_FIELDS else v)
+            if "rgba8" in fields:  # the colour pass's display buffer of frame i
+                v = torch.from_numpy(abi.rgba8_from_rgb(*(part[f] * (i + 1)
+                                                          for f in RGB_FIELDS)))
+                fb.views["rgba8"][:len(v)].copy_(v)
             pipe.submit()
         fr = pipe.finish()
         if rank == 0:
@@ -98,6 +105,34 @@ def test_gloo_tiles_reassemble_frame(tmp_path, oracle, world, W, H, B, gather, f
     idx = shard_rows_index(H, B, 0, world)
     assert np.array_equal(got["local_rows"], idx)
     assert np.array_equal(got["loc_steps"], want["steps"].reshape(H, W)[idx])
+
+
+@pytest.mark.parametrize("world,W,H,B,S,frames", [
+    (2, 24, 32, 4, 2, 1), (3, 16, 26, 4, 3, 3), (2, 16, 40, 2, 4, 2)])
+def test_gloo_rgba8_gather_assembles_display_image(tmp_path, oracle, world, W, H, B, S,
+                                                   frames):
+    """bench.py's default exchange: ONE gather of the 4-byte rgba8 display buffer (not the
+    24-byte f64 colour planes). Rank 0's image is the rendered shards' display pixels, within
+    one 8-bit step of the oracle's f64 colour; rows of shards no rank rendered stay 0."""
+    got = _run_tiles(tmp_path, world, W, H, B, S, "rgba8", frames)
+    assert sorted(k for k in got if k.startswith("img_")) == ["img_rgba8"]
+    img = got["img_rgba8"]
+    assert img.shape == (H, W, 4) and img.dtype == np.uint8
+    want = _c2_frame(oracle, W, H)
+    mine = np.concatenate([shard_rows_index(H, B, s, S) for s in range(world)])
+    rgb = [want[f].reshape(H, W)[mine] * frames for f in RGB_FIELDS]
+    assert np.array_equal(img[mine], abi.rgba8_from_rgb(*rgb))
+    for i, v in enumerate(rgb):  # one 8-bit step of the f64 colour (NaN -> 255)
+        ref = np.where(np.isnan(v), 255.0, np.minimum(v, 1.0) * 255.0)
+        assert np.all(np.abs(img[mine][..., i] - ref) <= 1.0)
+    assert not np.delete(img, mine, axis=0).any()
+    # rank 0 keeps its own shard's f64 SoA (the per-ray record stays resident per rank)
+    idx = shard_rows_index(H, B, 0, S)
+    assert np.array_equal(got["loc_steps"], want["steps"].reshape(H, W)[idx])
+    # exchange size: 4 B per ray instead of 24
+    fb = FrameBuffer(8, "cpu", abi.SOA_FIELDS + DISPLAY_FIELD)
+    a, b = fb.span(DISPLAY_FIELD)
+    assert b - a == 4 * 8 and fb.span(RGB_FIELDS)[1] - fb.span(RGB_FIELDS)[0] == 24 * 8
 
 
 def test_gloo_partial_node_frame(tmp_path, oracle):
@@ -276,3 +311,7 @@ def test_framebuffer_alignment_and_colour_tail():
         assert b == fb.nbytes and b - a == 24 * n
     with pytest.raises(ValueError):
         FrameBuffer(4, "cpu").span(("result", "rgb_r"))
+    fb = FrameBuffer(5, "cpu", abi.SOA_FIELDS + DISPLAY_FIELD)
+    assert fb.views["rgba8"].shape == (5, 4) and fb.views["rgba8"].dtype == torch.uint8
+    assert fb.offsets["rgba8"][1] <= min(fb.offsets[f][0] for f in RGB_FIELDS)
+    assert all(fb.offsets[f][0] % 8 == 0 for f in RGB_FIELDS)

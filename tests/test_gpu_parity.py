@@ -19,10 +19,6 @@ from bhrt import abi, configs
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-5
-# Host arrays that libbhrt page-locked (BHRT_HOST_REGISTER=1) stay allocated until the process
-# ends: the HIP runtime keeps its record of a registered range past hipHostUnregister, and a
-# later pageable copy into memory re-using that address range would follow the stale record.
-_PAGE_LOCKED = []
 
 
 @pytest.mark.parametrize("name", golden_names("frame_"))
@@ -494,8 +490,6 @@ def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch, register):
     for chunks in ("1", "3", "4", "8"):
         monkeypatch.setenv("BHRT_HOST_CHUNKS", chunks)
         got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
-        if register:
-            _PAGE_LOCKED.append(got)
         for f in abi.SOA_FIELDS:
             assert np.array_equal(got[f], ref[f], equal_nan=True), (chunks, f)
 
@@ -555,15 +549,15 @@ def test_async_frames_in_flight_equal_sync_frames(bhrt_lib, monkeypatch, registe
                                              C.byref(t)) == 0, bhrt_lib.last_error()
             tickets.append(t.value)
         assert len(set(tickets)) == 4 and min(tickets) > 0
-        # the fourth issue reused the first slot: frame 1 was waited for implicitly
-        assert L.bhrt_frame_wait(tickets[0]) == -1
-        for t in tickets[1:]:
+        # the fourth issue took the oldest frame's slot and completed frame 1 first; frame
+        # 1's own wait still returns its result, once
+        for t in tickets:
             assert L.bhrt_frame_wait(t) == 0, bhrt_lib.last_error()
-        assert L.bhrt_frame_wait(tickets[-1]) == -1  # already waited for
+        assert L.bhrt_frame_wait(tickets[0]) == -1  # already waited for
+        assert L.bhrt_frame_wait(tickets[-1]) == -1
         assert L.bhrt_frame_wait(max(tickets) + 100) == -1
     finally:
         assert hip.hipHostUnregister(pre.ctypes.data) == 0  # still the caller's registration
-    _PAGE_LOCKED.append((outs, keep))  # (the caller-registered `pre` array too)
     for (cname, camname), (arrays, _) in zip(jobs, outs):
         c = configs.CONFIGS[cname]
         bh, dk, cfg = c.scene()
@@ -571,6 +565,81 @@ def test_async_frames_in_flight_equal_sync_frames(bhrt_lib, monkeypatch, registe
                                      c.flags, fields=tuple(arrays))
         for f in arrays:
             assert np.array_equal(arrays[f], want[f], equal_nan=True), (cname, camname, f)
+
+
+def test_registered_frames_with_freed_arrays_and_pageable_copies(bhrt_lib, monkeypatch):
+    """BHRT_HOST_REGISTER=1 as a render loop that reallocates uses it: every frame's caller
+    arrays are freed right after the frame (some carved out of one allocation at odd
+    offsets, some small enough to come from the heap next to other allocations), two frames
+    in flight, and after every frame pageable torch D2H copies and heap allocations that
+    re-use the freed memory. libbhrt page-locks only whole pages inside each array (DESIGN.md
+    section 4), so no other allocation can start in a locked page; every frame must equal the
+    device frame and every pageable copy its source."""
+    import torch
+    monkeypatch.setenv("BHRT_HOST_REGISTER", "1")
+    L = bhrt_lib.load()
+    c = configs.CONFIGS["C2"]
+    bh, dk, cfg = c.scene()
+    cams = [configs.camera("B"), configs.camera("A")]
+    W, H = 768, 432  # 332 k rays, 32 MB of fields: the DMA path, 2 chunks
+    refs = []
+    for cam in cams:
+        t = {f: torch.zeros(W * H, dtype=torch.int32 if f in ("result", "steps") else
+                            torch.float64, device="cuda") for f in abi.SOA_FIELDS}
+        bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                     bhrt_lib.soa_from_tensors(t), 0)
+        torch.cuda.synchronize()
+        refs.append({f: v.cpu().numpy() for f, v in t.items()})
+    src = torch.arange(1 << 18, dtype=torch.float64, device="cuda")
+    for it in range(6):
+        junk = [np.full(777 + 13 * k, k, dtype=np.uint8) for k in range(64)]  # heap neighbours
+        sets = []
+        for j in range(2):
+            if (it + j) % 2:
+                buf, arrays, soa = _frame_soa_in_one_buffer(W * H, abi.SOA_FIELDS,
+                                                            offset=(1000 * it + 24 * j) % 4096)
+            else:
+                buf = None
+                arrays, soa = abi.alloc_soa(W * H)
+            sets.append((buf, arrays, soa))
+        tickets = []
+        for j, (_, _, soa) in enumerate(sets):
+            t = C.c_int(0)
+            cam = cams[j]
+            assert L.bhrt_render_frame_async(C.byref(bh), C.byref(dk), C.byref(cfg),
+                                             C.byref(cam), W, H, c.method, c.flags,
+                                             C.byref(soa), C.byref(t)) == 0, bhrt_lib.last_error()
+            tickets.append(t.value)
+        for t in tickets:
+            assert L.bhrt_frame_wait(t) == 0, bhrt_lib.last_error()
+        for j, (_, arrays, _) in enumerate(sets):
+            for f in abi.SOA_FIELDS:
+                assert np.array_equal(arrays[f], refs[j][f], equal_nan=True), (it, j, f)
+        del sets, arrays, soa, buf
+        for k in range(8):  # pageable copies into freshly allocated (recycled) host memory
+            n = (1 << 12) << k
+            host = src[:n].cpu()
+            assert host[-1].item() == n - 1 and bool((host[:7] == src[:7].cpu()).all())
+        del junk
+
+
+def test_small_claimed_launches(bhrt_lib, oracle):
+    """Launches of a few workgroups on the block-claim paths (Kerr / RKF45 scenes: claim_div
+    1): the claim-size shift is computed for grids smaller than the queue count too."""
+    g = golden("rays_rkf45_kerr")
+    bh, dk, cfg = scene_from(g)
+    rays = rays_from(g)
+    for n in (1, 3, 64, 65, 700):
+        sub = np.resize(rays, n)
+        got = bhrt_lib.trace_rays(sub, bh, dk, cfg, int(g["method"]), int(g["flags"]))
+        want = oracle.trace_rays(sub, bh, dk, cfg, int(g["method"]), int(g["flags"]))
+        compare(got, want, RTOL, sky_pinned(g["method"]), f"n={n}")
+    c = configs.CONFIGS["C4"]
+    bh, dk, cfg = c.scene()
+    for W, H in ((4, 3), (40, 17)):
+        got = bhrt_lib.render_frame(bh, dk, cfg, configs.camera("B"), W, H, c.method, c.flags)
+        want = oracle.render_frame(bh, dk, cfg, configs.camera("B"), W, H, c.method, c.flags)
+        compare(got, want, RTOL, False, f"C4 {W}x{H}")
 
 
 @pytest.mark.parametrize("n", [65536, 300_001, (1 << 20) + 7])  # 4, 4 and 8 chunks
