@@ -361,46 +361,54 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
     """bhrt_render_frame into host SoA arrays (allocated and touched once, reused every frame
     as a render loop does): the PCIe-inclusive rate a C caller of the host API sees, one
     synchronous call per frame, and with bhrt_render_frame_async three frames in flight (three
-    sets of host arrays; frame i+1 traces while frame i is copied). Also the latency of one
-    drop-in trace_ray call. Reported beside `value`, never as it."""
+    sets of host arrays; frame i+1 traces while frame i is copied) -- for every SoA field (96
+    B/ray) and for the visualizer's display call, the rgba8 buffer alone (4 B/px,
+    INTEGRATION.md). Also the reference batch API and the latency of one drop-in trace_ray
+    call. Reported beside `value`, never as it."""
     import ctypes as C
     L = lib.load()
     depth = 3  # frames in flight (bhrt_render_frame_async keeps up to 3 per thread)
-    sets = [abi.alloc_soa(W * H) for _ in range(depth)]
-    for arrays, _ in sets:
-        for a in arrays.values():
-            a[...] = 0
     args = (C.byref(bh), C.byref(dk) if dk else None, C.byref(cfg), C.byref(cam), W, H,
             c.method, c.flags)
 
-    def sync_frame():
-        if L.bhrt_render_frame(*args, C.byref(sets[0][1])) != 0:
-            raise RuntimeError(lib.last_error())
+    def leg(fields):
+        sets = [abi.alloc_soa(W * H, fields) for _ in range(depth)]
+        for arrays, _ in sets:
+            for a in arrays.values():
+                a[...] = 0
 
-    def issue(i):
-        t = C.c_int(0)
-        if L.bhrt_render_frame_async(*args, C.byref(sets[i % depth][1]), C.byref(t)) != 0:
-            raise RuntimeError(lib.last_error())
-        return t.value
+        def sync_frame():
+            if L.bhrt_render_frame(*args, C.byref(sets[0][1])) != 0:
+                raise RuntimeError(lib.last_error())
 
-    def wait(t):
-        if L.bhrt_frame_wait(t) != 0:
-            raise RuntimeError(lib.last_error())
+        def issue(i):
+            t = C.c_int(0)
+            if L.bhrt_render_frame_async(*args, C.byref(sets[i % depth][1]), C.byref(t)) != 0:
+                raise RuntimeError(lib.last_error())
+            return t.value
 
-    for _ in range(depth):  # the library's three frame slots each allocate their pinned
-        sync_frame()         # staging on first use: steady state, as in a render loop
-    t0 = time.perf_counter()
-    for _ in range(frames):
-        sync_frame()
-    dt = (time.perf_counter() - t0) / frames
-    wait(issue(0))
-    t0 = time.perf_counter()
-    pending = [issue(i) for i in range(depth - 1)]
-    for i in range(depth - 1, frames + depth - 1):
-        if i < frames:
-            pending.append(issue(i))
-        wait(pending.pop(0))
-    dta = (time.perf_counter() - t0) / frames
+        def wait(t):
+            if L.bhrt_frame_wait(t) != 0:
+                raise RuntimeError(lib.last_error())
+
+        sync_frame()  # the slot's buffers and pinned staging allocated on first use
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            sync_frame()
+        dt = (time.perf_counter() - t0) / frames
+        for t in [issue(i) for i in range(depth)]:  # every slot warm
+            wait(t)
+        t0 = time.perf_counter()
+        pending = [issue(i) for i in range(depth - 1)]
+        for i in range(depth - 1, frames + depth - 1):
+            if i < frames:
+                pending.append(issue(i))
+            wait(pending.pop(0))
+        dta = (time.perf_counter() - t0) / frames
+        return dt, dta, sum(a.nbytes for a in sets[0][0].values())
+
+    dt, dta, nbytes = leg(FIELDS)
+    dt8, dta8, nbytes8 = leg(("rgba8",))
     # the reference's batch API (trace_rays_batch: Ray[] in, 160-byte RayTraceHit[] out, only
     # the fields trace_ray writes) on the frame's camera rays, arrays reused
     batch = None
@@ -428,14 +436,19 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
     return {"mrays_s": round(W * H / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 3),
             "async_mrays_s": round(W * H / dta / 1e6, 3),
             "async_ms_per_frame": round(dta * 1e3, 3),
-            "bytes_to_host_per_frame": W * H * 96,
+            "bytes_to_host_per_frame": nbytes,
+            "rgba8_mrays_s": round(W * H / dt8 / 1e6, 3),
+            "rgba8_ms_per_frame": round(dt8 * 1e3, 3),
+            "rgba8_async_mrays_s": round(W * H / dta8 / 1e6, 3),
+            "rgba8_bytes_to_host_per_frame": nbytes8,
             "trace_rays_batch_mrays_s": batch,
             "trace_ray_latency_ms": round(sorted(lat[2:])[len(lat[2:]) // 2] * 1e3, 3),
             "note": "bhrt_render_frame into reused host arrays (every field; pinned staging, "
-                    "host un-permute by up to 16 threads); async = bhrt_render_frame_async with three frames "
-                    "in flight; trace_rays_batch = the reference batch API on the frame's camera "
-                    "rays (RayTraceHit[] out); trace_ray = median of one drop-in call, PCIe "
-                    "round trip included"}
+                    "host un-permute by up to 16 threads); async = bhrt_render_frame_async with "
+                    "three frames in flight; rgba8 = the same calls with only the display buffer "
+                    "(the visualizer's call, INTEGRATION.md); trace_rays_batch = the reference "
+                    "batch API on the frame's camera rays (RayTraceHit[] out); trace_ray = median "
+                    "of one drop-in call, PCIe round trip included"}
 
 
 def pmc_profile(config):

@@ -99,6 +99,26 @@ void orc_initialize_black_hole_params(BlackHoleParams* bh, double mass, double s
     bh->isco_radius = isco_radius(bh);
 }
 
+/* ---- knife-edge margins; off unless orc_render_frame_margin runs ----
+ * For every DISCONTINUOUS decision a ray takes (step-size schedule, far-field switch,
+ * horizon and distance exits, RKF45 accept, the pole clamp's sign, the disk test's
+ * |denominator| threshold, t sign and radii), the relative distance of the tested value from
+ * its threshold; a ray's margin is the smallest over the decisions that reach its pinned
+ * outputs (for a disk hit at segment i: iterations 1..i and segments 1..i). Continuous clamps
+ * (|d| <= 10, r >= 1.5 rs, |sin| >= 0.01) are not decisions in this sense. A ray whose margin
+ * is below ~1e-9 can change class or step count under a last-bit difference of its inputs.
+ * Tracking never changes a computed value. */
+static _Thread_local int g_mg_on;
+static _Thread_local double g_mg;       /* running minimum of the current ray */
+static _Thread_local double* g_mg_iter; /* [k] = g_mg after the iteration that stored path[k] */
+static _Thread_local double g_mg_result;
+static void mg_note(double m) {
+    if (g_mg_on && m < g_mg) g_mg = m; /* (NaN comparisons decide the same everywhere) */
+}
+static void mg_rel(double a, double b) {
+    if (g_mg_on) mg_note(fabs(a - b) / fabs(b));
+}
+
 /* ---- raytracer.c:19-33 integration parameters ---- */
 typedef struct {
     const BlackHoleParams* bh;
@@ -115,6 +135,7 @@ static void orc_derivs(const double s[], double d[], const OrcRay* p, int n) {
     double v_r = s[3], v_theta = s[4], v_phi = s[5];
     d[0] = v_r; d[1] = v_theta; d[2] = v_phi;
     if (n > 6) { d[6] = 0.0; d[7] = 0.0; } /* convention, see file header */
+    if (p->use_analytic_approx) mg_rel(r, p->field_strength_threshold);
     if (p->use_analytic_approx && r > p->field_strength_threshold) { /* :65-86 */
         double M = p->bh->mass;
         double deflection_factor = 2.0 * M / (r * r);
@@ -132,6 +153,7 @@ static void orc_derivs(const double s[], double d[], const OrcRay* p, int n) {
         double sin_theta_sq = sin_theta * sin_theta;
         if (r <= rs * 1.5) { r = rs * 1.5; r_sq = r * r; }
         if (fabs(sin_theta) < 0.01) {
+            mg_note(fabs(sin_theta)); /* the clamp's sign flips at sin = 0 */
             sin_theta = (sin_theta >= 0.0) ? 0.01 : -0.01;
             sin_theta_sq = sin_theta * sin_theta;
         }
@@ -202,6 +224,7 @@ static int orc_rkf45(double y[], int n, double h, double eps_rel, const OrcRay* 
         max_error = fmax(max_error, error);
     }
     double error_ratio = max_error / eps_rel;
+    mg_rel(error_ratio, 1.0);
     if (error_ratio <= 1.0) { /* :402-434 (t and h_next are not used by the caller) */
         for (int i = 0; i < n; i++) y[i] = y5[i];
         return 0;
@@ -242,6 +265,7 @@ RayTraceResult orc_integrate_photon_path(const Vector4D* position, const Vector3
                      sin(theta) * nd.z) / r;
     double dphi = (-sin(phi) * nd.x + cos(phi) * nd.y) / (r * sin(theta));
     if (fabs(sin(theta)) < BH_EPSILON) dphi = 0.0; /* :402-405 */
+    mg_rel(fabs(sin(theta)), BH_EPSILON);
     SchwarzschildMetric m = schw_metric(r, bh); /* :412 */
     double dt_squared = -(m.g_rr * dr * dr + m.g_thth * dtheta * dtheta +
                           m.g_phph * dphi * dphi) / m.g_tt;
@@ -255,17 +279,26 @@ RayTraceResult orc_integrate_photon_path(const Vector4D* position, const Vector3
     rp.impact_parameter = fabs(angular_momentum / energy);
     rp.field_strength_threshold = bh->schwarzschild_radius * 15.0; /* :465-466 */
     rp.use_analytic_approx = (r > rp.field_strength_threshold) ? 1 : 0;
+    mg_rel(r, rp.field_strength_threshold);
+    if (rp.use_analytic_approx) mg_note(rp.impact_parameter / r); /* b > 0 selects the branch */
 
     int step_count = 0;
     double distance_traveled = 0.0;
     Vector3D current_pos, sph0 = {state[1], state[2], state[3]};
     sph2cart(&sph0, &current_pos); /* :501 */
     if (path != NULL && max_positions > 0) { path[0] = current_pos; *num_positions = 1; }
+    if (g_mg_iter && path != NULL && max_positions > 0) g_mg_iter[0] = g_mg;
     RayTraceResult result = RAY_MAX_STEPS;
     while (step_count < cfg->max_integration_steps) { /* :517-665 */
         for (int i = 0; i < 8; i++) /* :543-548 */
             if (isnan(state[i]) || isinf(state[i])) state[i] = (i < 4) ? 1.0 : 0.0;
         double h; /* :556-571 */
+        if (g_mg_on) { /* the comparisons the chain evaluates */
+            const double rs = bh->schwarzschild_radius;
+            mg_rel(state[1], rs * 2.5);
+            if (!(state[1] < rs * 2.5)) mg_rel(state[1], rs * 5.0);
+            if (!(state[1] < rs * 5.0)) mg_rel(state[1], rs * 15.0);
+        }
         if (state[1] < bh->schwarzschild_radius * 2.5) h = cfg->time_step * 0.001;
         else if (state[1] < bh->schwarzschild_radius * 5.0) h = cfg->time_step * 0.01;
         else if (state[1] < bh->schwarzschild_radius * 15.0) h = cfg->time_step * 0.1;
@@ -281,9 +314,16 @@ RayTraceResult orc_integrate_photon_path(const Vector4D* position, const Vector3
         double step_distance = v_len(v_sub(np, current_pos)); /* :633-640 */
         current_pos = np;
         distance_traveled += step_distance;
+        int stored = -1;
         if (path != NULL && *num_positions < max_positions) { /* :643-646 */
             path[*num_positions] = current_pos;
-            (*num_positions)++;
+            stored = (*num_positions)++;
+        }
+        if (g_mg_on) {
+            mg_rel(state[1], bh->schwarzschild_radius * 1.05);
+            if (!(state[1] <= bh->schwarzschild_radius * 1.05))
+                mg_rel(distance_traveled, cfg->max_ray_distance);
+            if (g_mg_iter && stored >= 0) g_mg_iter[stored] = g_mg;
         }
         if (state[1] <= bh->schwarzschild_radius * 1.05) { result = RAY_HORIZON; break; }
         if (distance_traveled >= cfg->max_ray_distance) { result = RAY_MAX_DISTANCE; break; }
@@ -299,11 +339,21 @@ int orc_check_disk_intersection(const Vector3D* position, const Vector3D* veloci
                                 const Vector3D* disk_normal, const AccretionDiskParams* disk,
                                 Vector3D* hit_position) {
     double denom = v_dot(*velocity, *disk_normal);
+    if (g_mg_on) {
+        const double vn = v_len(*velocity) * v_len(*disk_normal);
+        mg_rel(fabs(denom), BH_EPSILON);
+        mg_note(fabs(denom) / vn);                                  /* t's sign: den's sign */
+        mg_note(fabs(v_dot(*position, *disk_normal)) / (v_len(*position) * v_len(*disk_normal)));
+    }
     if (fabs(denom) < BH_EPSILON) return 0;
     double t = -(v_dot(*position, *disk_normal)) / denom;
     if (t < 0.0) return 0;
     *hit_position = v_add(*position, v_scale(*velocity, t));
     double r = sqrt(hit_position->x * hit_position->x + hit_position->y * hit_position->y);
+    if (g_mg_on) {
+        mg_rel(r, disk->inner_radius);
+        if (r >= disk->inner_radius) mg_rel(r, disk->outer_radius);
+    }
     return (r >= disk->inner_radius && r <= disk->outer_radius) ? 1 : 0;
 }
 
@@ -318,12 +368,21 @@ RayTraceResult orc_trace_ray_method(const Ray* ray, const BlackHoleParams* bh,
         max_positions = cfg->max_integration_steps;
         path = (Vector3D*)malloc((size_t)(max_positions > 0 ? max_positions : 1) * sizeof(Vector3D));
     }
+    if (g_mg_on) {
+        g_mg = INFINITY;
+        g_mg_iter = path ? (double*)malloc((size_t)(max_positions > 0 ? max_positions : 1) *
+                                           sizeof(double)) : NULL;
+    }
     RayTraceResult result = orc_integrate_photon_path(&position, &ray->direction, bh, cfg, method,
                                                       path, max_positions, &num_positions, hit);
+    const double mg_path = g_mg;
+    if (g_mg_on) g_mg = INFINITY; /* from here: the disk tests of the scanned segments */
+    int hit_at = 0;
     if (disk != NULL && path != NULL && num_positions > 1) { /* :717-759 */
         for (int i = 1; i < num_positions; i++) {
             Vector3D q;
             if (orc_check_disk_intersection(&path[i], &ray->direction, &path[i - 1], disk, &q)) {
+                hit_at = i;
                 if (hit != NULL) {
                     hit->result = RAY_DISK;
                     hit->hit_position = q;
@@ -338,6 +397,12 @@ RayTraceResult orc_trace_ray_method(const Ray* ray, const BlackHoleParams* bh,
                 break;
             }
         }
+    }
+    if (g_mg_on) {
+        const double m_int = hit_at && g_mg_iter ? g_mg_iter[hit_at] : mg_path;
+        g_mg_result = m_int < g_mg ? m_int : g_mg;
+        free(g_mg_iter);
+        g_mg_iter = NULL;
     }
     free(path);
     return result;
@@ -592,10 +657,10 @@ static void trace_one(const Ray* ray, const BlackHoleParams* bh, const Accretion
     orc_trace_ray_method(ray, bh, disk, cfg, method, h); /* disk == NULL: plain integration */
 }
 
-int orc_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* disk,
-                     const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
-                     const bhrt_rows* rows, IntegrationMethod method, int flags,
-                     const bhrt_frame_soa* out, int nthreads) {
+static int render_frame(const BlackHoleParams* bh, const AccretionDiskParams* disk,
+                        const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                        const bhrt_rows* rows, IntegrationMethod method, int flags,
+                        const bhrt_frame_soa* out, double* margin, int nthreads) {
     if (!bh || !cfg || !cam || !out || W <= 0 || H <= 0) return -1;
     long n = (long)orc_shard_rows(H, rows) * W;
 #ifdef _OPENMP
@@ -611,12 +676,29 @@ int orc_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* disk,
                                  cam->use_offset ? cam->offset_y : 0.5, W, H, cam, &dir);
         Ray ray = {cam->position, dir};
         RayTraceHit h;
+        g_mg_on = margin != NULL;
         trace_one(&ray, bh, disk, cfg, method, &h);
+        if (margin) margin[i] = g_mg_result;
+        g_mg_on = 0;
         double rgb[3];
         frame_colour(h.result, &h.hit_position, &dir, bh, disk, flags, rgb);
         store(out, i, &h, rgb);
     }
     return 0;
+}
+
+int orc_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* disk,
+                     const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                     const bhrt_rows* rows, IntegrationMethod method, int flags,
+                     const bhrt_frame_soa* out, int nthreads) {
+    return render_frame(bh, disk, cfg, cam, W, H, rows, method, flags, out, NULL, nthreads);
+}
+
+int orc_render_frame_margin(const BlackHoleParams* bh, const AccretionDiskParams* disk,
+                            const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                            const bhrt_rows* rows, IntegrationMethod method, int flags,
+                            const bhrt_frame_soa* out, double* margin, int nthreads) {
+    return render_frame(bh, disk, cfg, cam, W, H, rows, method, flags, out, margin, nthreads);
 }
 
 int orc_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,

@@ -54,6 +54,11 @@ int orc_render_frame(const BlackHoleParams* bh, const AccretionDiskParams* disk,
                      const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
                      const bhrt_rows* rows, IntegrationMethod method, int flags,
                      const bhrt_frame_soa* out, int nthreads);
+/* the same frame, plus each ray's knife-edge margin (oracle.c "knife-edge margins") */
+int orc_render_frame_margin(const BlackHoleParams* bh, const AccretionDiskParams* disk,
+                            const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                            const bhrt_rows* rows, IntegrationMethod method, int flags,
+                            const bhrt_frame_soa* out, double* margin, int nthreads);
 int orc_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
                    const AccretionDiskParams* disk, const SimulationConfig* cfg,
                    IntegrationMethod method, int flags, const bhrt_frame_soa* out, int nthreads);

@@ -58,6 +58,22 @@ class Checker:
         assert rc == 0
         return arrays
 
+    def render_frame_margin(self, bh, dk, cfg, cam, width, height, method=abi.INTEGRATOR_RK4,
+                            flags=0, rows=None, threads=0, fields=abi.SOA_FIELDS):
+        """render_frame plus every ray's knife-edge margin (oracle only; oracle.c "knife-edge
+        margins"): returns (arrays, margin)."""
+        fn = self.lib.orc_render_frame_margin
+        fn.argtypes = _FRAME_ARGS[:-1] + [C.c_void_p, C.c_int]
+        fn.restype = C.c_int
+        n = width * (height if rows is None else _shard_rows(height, rows))
+        arrays, soa = abi.alloc_soa(n, fields)
+        margin = np.empty(n, dtype=np.float64)
+        rc = fn(C.byref(bh), C.byref(dk) if dk else None, C.byref(cfg), C.byref(cam), width,
+                height, C.byref(rows) if rows else None, method, flags, C.byref(soa),
+                margin.ctypes.data, threads)
+        assert rc == 0
+        return arrays, margin
+
     def trace_rays(self, rays, bh, dk, cfg, method=abi.INTEGRATOR_RK4, flags=0, threads=0,
                    fields=abi.SOA_FIELDS):
         rays = np.ascontiguousarray(rays, dtype=abi.RAY_DTYPE)

@@ -182,6 +182,13 @@ static int env_int(const char* name, int dflt) {
     return v ? atoi(v) : dflt;
 }
 
+/* Where the trace kernel writes the colour outputs at each ray's exit, from the state in
+ * registers (bhrt_colour_in_trace), the separate pass's inputs -- result and hit point -- need
+ * not exist on the device. BHRT_FUSE_COLOUR=0 keeps the separate colour pass (A/B). */
+static int colour_fused(int method, int has_disk) {
+    return BHRT_COLOUR_IN_TRACE(method, has_disk) && env_int("BHRT_FUSE_COLOUR", 1) != 0;
+}
+
 static void claim_policy(bhrt_kparams* kp) {
     int q = env_int("BHRT_QUEUES", 16), bits = 0;
     while (bits < BHRT_MAX_QUEUE_BITS && (2 << bits) <= q) bits++;
@@ -415,6 +422,7 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
     }
     kp->refill = g_refill ? g_refill : refill_default(s);
     claim_policy(kp);
+    kp->colour_fused = colour_fused((int)method, dk != NULL);
     kp->cam.rows.row_block = 1;
     kp->cam.rows.num_shards = 1;
     return 0;
@@ -538,13 +546,14 @@ static int check_scene(const BlackHoleParams* bh, const SimulationConfig* cfg) {
 }
 
 /* the colour pass (rgb and/or the display fields) reads result and the hit point */
-static int colour_args_bad(const bhrt_frame_soa* out) {
+static int colour_args_bad(const bhrt_frame_soa* out, int method, int has_disk) {
     if ((out->rgb_r || out->rgb_g || out->rgb_b) && !(out->rgb_r && out->rgb_g && out->rgb_b)) {
         set_err("rgb output needs all of rgb_r/g/b");
         return 1;
     }
-    if ((out->rgb_r || out->rgba32f || out->rgba8) && (!out->result || !out->hit_x || !out->hit_y)) {
-        set_err("colour outputs need result and hit_x/hit_y");
+    if ((out->rgb_r || out->rgba32f || out->rgba8) && !colour_fused(method, has_disk) &&
+        (!out->result || !out->hit_x || !out->hit_y)) {
+        set_err("colour outputs need result and hit_x/hit_y (separate colour pass)");
         return 1;
     }
     return 0;
@@ -566,7 +575,7 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
     int dev = current_device();
     devctx_t* c = ctx_get(dev);
     if (!c) return -1;
-    if (colour_args_bad(out)) return -1;
+    if (colour_args_bad(out, (int)method, dk != NULL)) return -1;
     void* scratch = stream_scratch(c, stream ? (hipStream_t)stream : c->stream,
                                    (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) *
                                        (size_t)nrows * (size_t)W);
@@ -592,7 +601,7 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
         if (!g_err[0]) set_err("invalid argument");
         return -1;
     }
-    if (colour_args_bad(out)) return -1;
+    if (colour_args_bad(out, (int)method, dk != NULL)) return -1;
     devctx_t* c = ctx_get(current_device());
     if (!c) return -1;
     void* scratch = stream_scratch(c, stream ? (hipStream_t)stream : c->stream,
@@ -614,11 +623,12 @@ static const size_t k_fsize[BHRT_NFIELDS] = {4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8,
 static void** soa_slot(bhrt_frame_soa* s, int f) { return ((void**)s) + f; }
 
 /* the fields a device SoA needs for the fields `want_in` requests */
-static bhrt_frame_soa device_fields(const bhrt_frame_soa* want_in) {
+static bhrt_frame_soa device_fields(const bhrt_frame_soa* want_in, int method, int has_disk) {
     bhrt_frame_soa want_buf = *want_in;
     if (want_buf.rgb_r || want_buf.rgb_g || want_buf.rgb_b) /* written together */
         want_buf.rgb_r = want_buf.rgb_g = want_buf.rgb_b = (double*)1;
-    if (want_buf.rgb_r || want_buf.rgba32f || want_buf.rgba8) { /* the colour pass reads these */
+    if ((want_buf.rgb_r || want_buf.rgba32f || want_buf.rgba8) && !colour_fused(method, has_disk)) {
+        /* the separate colour pass reads these */
         if (!want_buf.result) want_buf.result = (int32_t*)1;
         if (!want_buf.hit_x) want_buf.hit_x = (double*)1;
         if (!want_buf.hit_y) want_buf.hit_y = (double*)1;
@@ -644,8 +654,9 @@ static void soa_carve(char** p, const bhrt_frame_soa* fields, long n, bhrt_frame
 }
 
 /* carve a device SoA for n rays out of c->d_soa, for the fields `want` requests */
-static int device_soa(devctx_t* c, long n, const bhrt_frame_soa* want_in, bhrt_frame_soa* dev) {
-    const bhrt_frame_soa fields = device_fields(want_in);
+static int device_soa(devctx_t* c, long n, const bhrt_frame_soa* want_in, int method,
+                      int has_disk, bhrt_frame_soa* dev) {
+    const bhrt_frame_soa fields = device_fields(want_in, method, has_disk);
     const size_t bytes = soa_bytes(&fields, n);
     if (ensure(&c->d_soa, &c->cap_soa, bytes ? bytes : 256, 0)) return -1;
     char* p = (char*)c->d_soa;
@@ -1037,7 +1048,7 @@ static int frame_enqueue(host_frame* f, const BlackHoleParams* bh, const Accreti
         HIP_TRY(hipSetDevice(0));
         for (int i = 0; i < 2 + 2 * BHRT_MAX_CHUNKS; i++) HIP_TRY(hipEventCreate(&f->t_ev[i]));
     }
-    const bhrt_frame_soa fields = device_fields(host);
+    const bhrt_frame_soa fields = device_fields(host, (int)method, dk != NULL);
     for (int d = 0; d < ndev; d++) { /* device buffers: every chunk of device d */
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
@@ -1206,7 +1217,7 @@ int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
         jobs[d].c = c;
         jobs[d].n = m;
         if (ensure(&c->d_rays, &c->cap_rays, (size_t)m * sizeof(Ray), 0)) return -1;
-        if (device_soa(c, m, host, &jobs[d].dev)) return -1;
+        if (device_soa(c, m, host, (int)method, dk != NULL, &jobs[d].dev)) return -1;
         HIP_TRY(hipMemcpyAsync(c->d_rays, rays + base[d], (size_t)m * sizeof(Ray),
                                hipMemcpyHostToDevice, c->stream));
         if (bhrt_trace_rays_device((const Ray*)c->d_rays, (int)m, bh, dk, cfg, method, flags,

@@ -57,6 +57,13 @@ typedef struct {
     int st_tiny;                     /* fabs(sin th0) < BH_EPSILON              */
 } bhrt_camera_k;
 
+/* Whether the trace kernel writes a scene's colour outputs at each ray's exit (no separate
+ * colour pass re-reading the hits): RKF45 scenes with a disk (C3: rays end after ~2 attempts,
+ * so the pass is a large share of the frame; +5% same-box). Elsewhere the separate pass runs
+ * on the other stream's tail and costs less than the colour code's registers in the trace
+ * loop (C4 -3.5%, C2/C5 neutral; profiles/r03_ab_kernel.txt). */
+#define BHRT_COLOUR_IN_TRACE(method, has_disk) ((method) == INTEGRATOR_RKF45 && (has_disk))
+
 typedef struct {
     bhrt_scene_k sc;
     int src;              /* BHRT_SRC_*                                       */
@@ -78,6 +85,8 @@ typedef struct {
     int queue_stride;     /* u64 words between queue heads (<= BHRT_QUEUE_STRIDE_MAX)     */
     int claim_shift;      /* set by the launcher per launch: a block claim is the queue's
                              remainder >> claim_shift, 2^claim_shift >= waves * claim_div / queues */
+    int colour_fused;     /* the trace kernel writes the colour outputs (rgb, rgba32f, rgba8)
+                             of each ray at its exit; else a separate colour pass runs */
 } bhrt_kparams;
 
 /* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and

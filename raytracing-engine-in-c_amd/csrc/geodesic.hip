@@ -576,7 +576,6 @@ __device__ __forceinline__ void trig_advance(double a, double x, double& s, doub
 // residual corrections) without its denormal scaling and Inf/0 class fix-up, which only
 // x < 2^-767 needs -- those lanes take the library sqrt.
 __device__ __forceinline__ double sqrt_nr(double x) {
-    if (__builtin_expect(!(x >= 0x1p-767), 0)) return sqrt(x);
     const double y = __builtin_amdgcn_rsq(x);
     double s = x * y, hy = y * 0.5;
     const double r = __builtin_fma(-hy, s, 0.5);
@@ -585,7 +584,10 @@ __device__ __forceinline__ double sqrt_nr(double x) {
     double e = __builtin_fma(-s, s, x);
     s = __builtin_fma(e, hy, s);
     e = __builtin_fma(-s, s, x);
-    return __builtin_fma(e, hy, s);
+    s = __builtin_fma(e, hy, s);
+    // one rare branch (not an if / else pair of exec-mask regions around both forms)
+    if (__builtin_expect(!(x >= 0x1p-767), 0)) s = sqrt(x);
+    return s;
 }
 
 __device__ __forceinline__ double len3(double x, double y, double z) {
@@ -754,31 +756,25 @@ __device__ __forceinline__ void ray_init_camera(Ray_& R, const bhrt_camera_k& cm
     R.k = 0;
 }
 
-// check_disk_intersection (raytracer.c:159-196), plane "normal" = previous path point.
-// Two exact shortcuts: t = num/den < 0 when the signs differ (and the quotient cannot
-// underflow), so the division is only formed for t >= 0; and the radial test compares s = qx^2 + qy^2 against
-// the host's thresholds instead of taking sqrt(s) (bhrt_api.c sqrt_lower/upper_bound).
-__device__ __forceinline__ bool disk_test(Ray_& R, double nx, double ny, double nz,
-                                          const Scene& sc) {
+// check_disk_intersection (raytracer.c:159-196), plane "normal" = previous path point n,
+// straight-line: every lane forms t, the candidate point and the radial test, and the four
+// rejections are ONE mask (a per-test early return became nested exec-mask regions, ~50 SALU
+// per iteration). The radial test compares s = qx^2 + qy^2 against the host's thresholds
+// instead of taking sqrt(s) (bhrt_api.c sqrt_lower/upper_bound). t = num * RN(1/den) for
+// |den| in [1e-10, 1e150) (a lane whose |den| < 1e-10 is rejected whatever its t); the IEEE
+// quotient, in a rare branch, otherwise (NaN den included). A t < 0 by signs (|num| > 0) is
+// negative here too, so the reference's rejection order is kept without a sign test.
+__device__ __forceinline__ bool disk_hit(const Ray_& R, double nx, double ny, double nz,
+                                         const Scene& sc, double& qx, double& qy, double& qz) {
     const double den = (R.dx * nx + R.dy * ny) + R.dz * nz;
-    if (fabs(den) < kEps) return false;
     const double num = -((R.px * nx + R.py * ny) + R.pz * nz);
-    const bool normal = fabs(den) < 1.0e150;
-    // t < 0 (|t| > 1e-300, so the quotient cannot underflow to -0, for which t < 0 is false)
-    if (normal && fabs(num) > 1.0e-150 && ((num < 0.0) != (den < 0.0))) return false;
-    const double t = normal ? div_nr(num, den, rcp_nr(den)) : num / den;
-    if (t < 0.0) return false;  // NaN num
-    const double qx = R.px + R.dx * t, qy = R.py + R.dy * t, qz = R.pz + R.dz * t;
+    double t = div_nr(num, den, rcp_nr(den));
+    if (__builtin_expect(!(fabs(den) < 1.0e150), 0)) t = num / den;
+    qx = R.px + R.dx * t;
+    qy = R.py + R.dy * t;
+    qz = R.pz + R.dz * t;
     const double s = qx * qx + qy * qy;
-    if (s >= sc.disk_in_sq && s <= sc.disk_out_sq) {
-        // the ray ends here: the hit point replaces the current point, so no extra
-        // loop-carried registers hold it (the caller reads it from R.px..pz; +0.9% on C2)
-        R.px = qx;
-        R.py = qy;
-        R.pz = qz;
-        return true;
-    }
-    return false;
+    return !(fabs(den) < kEps) & !(t < 0.0) & (s >= sc.disk_in_sq) & (s <= sc.disk_out_sq);
 }
 
 enum Term : int { T_NONE = 0, T_HORIZON, T_DISK, T_MAXDIST, T_MAXSTEPS };
@@ -786,6 +782,18 @@ enum Term : int { T_NONE = 0, T_HORIZON, T_DISK, T_MAXDIST, T_MAXSTEPS };
 struct HSel {  // the four step sizes of the schedule, hoisted out of the kernel argument block
     double far_, r15, r5, r2_5;
 };
+
+// x unchanged, but opaque to the optimiser: the four step sizes stay four register values
+// selected by v_cndmask. Left visible as loads, the select chain over them became ONE load at a
+// selected address, and the promoted step-size array an LDS table: a ds_read_b64 and an
+// lgkmcnt wait at the head of every iteration's dependency chain.
+__device__ __forceinline__ double opaque(double x) {
+    asm volatile("" : "+s"(x));
+    return x;
+}
+__device__ __forceinline__ HSel hsel_of(const Scene& sc) {
+    return HSel{opaque(sc.h_far), opaque(sc.h_15), opaque(sc.h_5), opaque(sc.h_2_5)};
+}
 
 // :543-548, state NaN/Inf recovery at the top of an iteration. One test of the sum
 // (non-finite if any component is, or on overflow); the per-component repair runs only then.
@@ -806,7 +814,7 @@ __device__ __forceinline__ void state_repair(Ray_& R, Counters* hc) {
 // hs: the step sizes in registers (k_trace), or NULL to read them from the scene.
 template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n,
-                                           const HSel* hs = nullptr) {
+                                           const HSel hs) {
     Counters* const hc = HUGE ? nullptr : &n;
     // Instantiations with repair_at_refill() run the recovery once, when the ray is loaded:
     // there a finite state stays finite.
@@ -814,18 +822,10 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     // step schedule (:556-571), written as selects so the first true test wins; fmin(h, 0.1)
     // is folded into the values (host)
     const double r = R.y[1];
-    double h;
-    if (hs) {
-        h = hs->far_;
-        h = (r < sc.rs_x15) ? hs->r15 : h;
-        h = (r < sc.rs_x5) ? hs->r5 : h;
-        h = (r < sc.rs_x2_5) ? hs->r2_5 : h;
-    } else {
-        h = sc.h_far;
-        h = (r < sc.rs_x15) ? sc.h_15 : h;
-        h = (r < sc.rs_x5) ? sc.h_5 : h;
-        h = (r < sc.rs_x2_5) ? sc.h_2_5 : h;
-    }
+    double h = hs.far_;
+    h = (r < sc.rs_x15) ? hs.r15 : h;
+    h = (r < sc.rs_x5) ? hs.r5 : h;
+    h = (r < sc.rs_x2_5) ? hs.r2_5 : h;
     bool moved = true;
     if (METHOD != INTEGRATOR_RK4) n.iters++;  // RK4: counted at termination (k_trace)
     Trig1 tr{R.y[1], R.s1, R.c1};
@@ -856,27 +856,52 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     R.py = y;
     R.pz = z;
     R.k++;
-    // segment k = (p_k, p_{k-1}) is stored and scanned by trace_ray iff k < max_steps
-    if (DISK && R.k < sc.max_steps && disk_test(R, ox, oy, oz, sc)) {
-        R.dist += len3(R.px - ox, R.py - oy, R.pz - oz);
-        return T_DISK;
-    }
-    if (R.y[1] <= sc.rs_x1_05) return T_HORIZON;
-    if (R.dist >= sc.max_dist) return T_MAXDIST;
-    if (!moved) {
-        // Fixed point: every later iteration repeats this one with p_j = p_{j-1} = p_k.
-        // Only the duplicate segment (p_k, p_k) is new, and only if p_k != p_{k-1}.
-        if (DISK && R.k + 1 < sc.max_steps && (x != ox || y != oy || z != oz) &&
-            disk_test(R, x, y, z, sc)) {
-            R.k++;
-            R.dist += len3(R.px - x, R.py - y, R.pz - z);
-            return T_DISK;
+    if constexpr (!DISK) {
+        // exits in the reference's order as early returns (without a disk test they are a
+        // short chain of rare branches; the select form below measured -0.9% on C5,
+        // profiles/r03_ab_kernel.txt)
+        if (R.y[1] <= sc.rs_x1_05) return T_HORIZON;
+        if (R.dist >= sc.max_dist) return T_MAXDIST;
+        if (!moved) {  // fixed point (below)
+            R.k = sc.max_steps;
+            return T_MAXSTEPS;
         }
-        R.k = sc.max_steps;
-        return T_MAXSTEPS;
+        return R.k >= sc.max_steps ? T_MAXSTEPS : T_NONE;
+    } else {
+        // the exits as selects (the reference's order: disk, horizon, distance, fixed point,
+        // step budget; a disk hit overrides the others below)
+        int term = (R.y[1] <= sc.rs_x1_05) ? T_HORIZON
+                 : (R.dist >= sc.max_dist) ? T_MAXDIST
+                 : (R.k >= sc.max_steps)   ? T_MAXSTEPS
+                                           : T_NONE;
+        // segment k = (p_k, p_{k-1}) is stored and scanned by trace_ray iff k < max_steps
+        double qx, qy, qz;
+        if (disk_hit(R, ox, oy, oz, sc, qx, qy, qz) & (R.k < sc.max_steps)) {
+            // the ray ends here: the hit point replaces the current point, so no extra
+            // loop-carried registers hold it (store_hit reads it from R.px..pz; +0.9% on C2)
+            R.px = qx;
+            R.py = qy;
+            R.pz = qz;
+            R.dist += len3(qx - ox, qy - oy, qz - oz);
+            term = T_DISK;
+        }
+        if (!moved && term == T_NONE) {
+            // Fixed point: every later iteration repeats this one with p_j = p_{j-1} = p_k.
+            // Only the duplicate segment (p_k, p_k) is new, and only if p_k != p_{k-1}.
+            if (R.k + 1 < sc.max_steps && (x != ox || y != oy || z != oz) &&
+                disk_hit(R, x, y, z, sc, qx, qy, qz)) {
+                R.px = qx;
+                R.py = qy;
+                R.pz = qz;
+                R.k++;
+                R.dist += len3(qx - x, qy - y, qz - z);
+                return T_DISK;
+            }
+            R.k = sc.max_steps;
+            return T_MAXSTEPS;
+        }
+        return term;
     }
-    if (R.k >= sc.max_steps) return T_MAXSTEPS;
-    return T_NONE;
 }
 
 // fill_hit_info (raytracer.c:299-333) / the disk branch of trace_ray (:728-753)
@@ -935,6 +960,118 @@ __device__ __forceinline__ void load_init(const bhrt_kparams& kp, int i, Ray_& R
     R.c3 = f[20 * n + i];
     R.dist = 0.0;
     R.k = 0;
+}
+
+__device__ __forceinline__ double clampd(double v, double lo, double hi) {
+    if (v < lo) return lo;  // math_util.c:505-509 (NaN passes through)
+    if (v > hi) return hi;
+    return v;
+}
+
+// Frame colour contract (DESIGN.md section 3), one elementwise pass after the trace:
+// calculate_disk_temperature + temperature_to_rgb (+ apply_relativistic_effects) for disk
+// hits, black for the horizon, the sky gradient of raytracer.c:1150-1157 otherwise.
+// (unsigned char)(std::min(1.0f, v) * 255.0f) as the visualizer's x86 build evaluates it:
+// std::min keeps 1.0f for NaN, the cast truncates toward zero and keeps the low byte.
+__device__ __forceinline__ unsigned to_u8(float v) {
+    const float m = (v < 1.0f) ? v : 1.0f;
+    return (unsigned)(int)(m * 255.0f) & 0xffu;
+}
+
+
+// The frame colour contract of one ray: calculate_disk_temperature +
+// temperature_to_rgb (+ apply_relativistic_effects with BHRT_FLAG_DOPPLER) of a disk hit at
+// (hx, hy), black for the horizon, the sky gradient of raytracer.c:1150-1157 on the ray
+// direction's y otherwise. Written by the trace kernel at the ray's exit (colour_fused) or by
+// the separate k_colour pass.
+__device__ __forceinline__ void colour_of(const Scene& sc, int res, double hx, double hy,
+                                          double dx, double dy, double dz, double& r,
+                                          double& g, double& b) {
+    if (res == RAY_DISK) {
+        const double rxy = sqrt(hx * hx + hy * hy);  // raytracer.c:201-228
+        double nr = (rxy - sc.disk_in) / (sc.disk_out - sc.disk_in);
+        nr = clampd(nr, 0.0, 1.0);
+        // pow(1 - nr, 0.75) as sqrt(u) * sqrt(sqrt(u)), u in [0, 1] (a few ulp: the colour
+        // contract's tolerance is 1e-5)
+        const double su = sqrt(1.0 - nr);
+        const double T = clampd(sc.disk_tscale * (2000.0 + 18000.0 * (su * sqrt(su))),
+                                1000.0, 40000.0);  // math_util.c:463-503
+        const double t = (T - 1000.0) / (40000.0 - 1000.0);
+        r = (t < 0.5) ? t * 2.0 : 1.0;
+        g = (t < 0.25) ? 0.0 : ((t < 0.75) ? (t - 0.25) * 2.0 : 1.0);
+        b = (t < 0.5) ? 0.0 : (t - 0.5) * 2.0;
+        const double br = 0.2 + 0.8 * (t * t);
+        r *= br;
+        g *= br;
+        b *= br;
+        if (sc.flags & BHRT_FLAG_DOPPLER) {  // raytracer.c:233-294
+            // sin, cos of atan2(hy, hx) as hy / rxy, hx / rxy (rxy > 0: a disk hit lies at
+            // rxy >= disk_in), pow(dop, 4) as two squarings, dop / (1 / sqrt(f)) as
+            // dop * sqrt(f): each within a few ulp of the libm forms
+            // (rxy = 0 -- a zero inner radius -- is atan2(+-0, +0) = +-0 or atan2(+-0, -0) =
+            // +-pi, whose sin, cos are (+-0, 1) and (+-RN(sin pi), -1): selects, no libm call
+            // in the trace kernel)
+            const double ir = 1.0 / rxy;
+            double sp = hy * ir, cp = hx * ir;
+            if (!(rxy > 0.0)) {
+                const bool neg_x = __builtin_signbit(hx);
+                sp = neg_x ? __builtin_copysign(1.2246467991473532e-16, hy) : hy;
+                cp = neg_x ? -1.0 : 1.0;
+            }
+            const double dop = 1.0 + ((dx * -sp + dy * cp) + dz * 0.0) * 0.5;
+            const double z = dop * sqrt(1.0 - sc.rs / rxy);
+            if (z < 1.0) {
+                b *= z;
+                r = fmin(1.0, r * (2.0 - z));
+            } else {
+                r *= 2.0 - z;
+                b = fmin(1.0, b * z);
+            }
+            const double d2 = dop * dop, beam = d2 * d2;
+            r = clampd(r * beam, 0.0, 1.0);
+            g = clampd(g * beam, 0.0, 1.0);
+            b = clampd(b * beam, 0.0, 1.0);
+        }
+    } else if (res == RAY_HORIZON) {
+        r = g = b = 0.0;
+    } else {
+        const double t = 0.5 * (dy + 1.0);
+        r = (1.0 - t) * 1.0 + t * 0.5;
+        g = (1.0 - t) * 1.0 + t * 0.7;
+        b = (1.0 - t) * 1.0 + t * 1.0;
+    }
+}
+
+__device__ __forceinline__ void store_colour(const bhrt_frame_soa& s, int i, double r, double g,
+                                             double b) {
+    if (s.rgb_r) {
+        s.rgb_r[i] = r;
+        s.rgb_g[i] = g;
+        s.rgb_b[i] = b;
+    }
+    if (s.rgba32f || s.rgba8) {  // the display path (renderer.cpp:2090-2125)
+        const float fr = (float)r, fg = (float)g, fb = (float)b;
+        if (s.rgba32f) reinterpret_cast<float4*>(s.rgba32f)[i] = make_float4(fr, fg, fb, 1.0f);
+        if (s.rgba8)
+            reinterpret_cast<unsigned*>(s.rgba8)[i] =
+                to_u8(fr) | (to_u8(fg) << 8) | (to_u8(fb) << 16) | (to_u8(1.0f) << 24);
+    }
+}
+
+// store_hit, and where the scene's colour is written in the trace kernel
+// (BHRT_COLOUR_IN_TRACE, bhrt_kernel.h; colour_fused) the colour outputs from the exit state in
+// registers. Other instantiations do not contain the colour code at all (its registers cost
+// more in the loop than the separate pass does).
+template <int METHOD, bool DISK>
+__device__ __forceinline__ void store_ray(const bhrt_kparams& kp, int i, const Ray_& R, int term) {
+    store_hit(kp.out, i, R, term, kp.sc);
+    if (!BHRT_COLOUR_IN_TRACE(METHOD, DISK)) return;
+    if (kp.colour_fused && (kp.out.rgb_r || kp.out.rgba32f || kp.out.rgba8)) {
+        const int res = term == T_DISK ? RAY_DISK : (term == T_HORIZON ? RAY_HORIZON : RAY_MAX_STEPS);
+        double r, g, b;
+        colour_of(kp.sc, res, R.px, R.py, R.dx, R.dy, R.dz, r, g, b);
+        store_colour(kp.out, i, r, g, b);
+    }
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
@@ -1079,7 +1216,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         s_q[wv][3] = 0u;
     }
     bool exhausted = false;  // no ids left to claim or hand out; wave-uniform
-    const HSel hsel{kp.sc.h_far, kp.sc.h_15, kp.sc.h_5, kp.sc.h_2_5};
+    const HSel hsel = hsel_of(kp.sc);
     for (;;) {
         const unsigned long long live_mask = __ballot(live);
         int n_live = __popcll(live_mask);
@@ -1177,7 +1314,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
-                        store_hit(kp.out, rid, R, T_MAXSTEPS, kp.sc);
+                        store_ray<METHOD, DISK>(kp, rid, R, T_MAXSTEPS);
                         live = false;
                     }
                 }
@@ -1189,14 +1326,14 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             continue;
         }
         if (live) {
-            int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, &hsel);
+            int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, hsel);
             // further iterations in the same trip for rays that go on: the loop's hand-over
             // copies between iterations (state, point, distance, carried sin/cos) fold away. A
             // lane's iterations are the same either way; only its refill point moves.
 #pragma unroll
             for (int u = 1; u < unroll_n<METHOD, SPIN0, HUGE>(); u++)
                 if (term == T_NONE && !n.huge)
-                    term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, &hsel);
+                    term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, hsel);
             if (METHOD == INTEGRATOR_RK4 && (term != T_NONE || (!HUGE && n.huge)))
                 n.iters += R.k;  // every RK4 iteration moves, so R.k = iterations executed
             if (!HUGE && n.huge) {  // hand the ray to the HUGE instantiation
@@ -1205,7 +1342,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 kp.redo[atomicAdd(kp.ctl + 6, 1ull)] = rid;
                 live = false;
             } else if (term != T_NONE) {
-                store_hit(kp.out, rid, R, term, kp.sc);
+                store_ray<METHOD, DISK>(kp, rid, R, term);
                 live = false;
             }
         }
@@ -1231,25 +1368,8 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     }
 }
 
-__device__ __forceinline__ double clampd(double v, double lo, double hi) {
-    if (v < lo) return lo;  // math_util.c:505-509 (NaN passes through)
-    if (v > hi) return hi;
-    return v;
-}
-
-// Frame colour contract (DESIGN.md section 3), one elementwise pass after the trace:
-// calculate_disk_temperature + temperature_to_rgb (+ apply_relativistic_effects) for disk
-// hits, black for the horizon, the sky gradient of raytracer.c:1150-1157 otherwise.
-// (unsigned char)(std::min(1.0f, v) * 255.0f) as the visualizer's x86 build evaluates it:
-// std::min keeps 1.0f for NaN, the cast truncates toward zero and keeps the low byte.
-__device__ __forceinline__ unsigned to_u8(float v) {
-    const float m = (v < 1.0f) ? v : 1.0f;
-    return (unsigned)(int)(m * 255.0f) & 0xffu;
-}
-
 template <int SRC>
 __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
-    const Scene& sc = kp.sc;
     const bhrt_frame_soa& s = kp.out;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += gridDim.x * blockDim.x) {
         double dx, dy, dz;
@@ -1262,70 +1382,9 @@ __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
         }
         const int res = s.result[i];
         double r, g, b;
-        if (res == RAY_DISK) {
-            const double hx = s.hit_x[i], hy = s.hit_y[i];
-            const double rxy = sqrt(hx * hx + hy * hy);  // raytracer.c:201-228
-            double nr = (rxy - sc.disk_in) / (sc.disk_out - sc.disk_in);
-            nr = clampd(nr, 0.0, 1.0);
-            // pow(1 - nr, 0.75) as sqrt(u) * sqrt(sqrt(u)), u in [0, 1] (a few ulp: the colour
-            // contract's tolerance is 1e-5)
-            const double su = sqrt(1.0 - nr);
-            const double T = clampd(sc.disk_tscale * (2000.0 + 18000.0 * (su * sqrt(su))),
-                                    1000.0, 40000.0);  // math_util.c:463-503
-            const double t = (T - 1000.0) / (40000.0 - 1000.0);
-            r = (t < 0.5) ? t * 2.0 : 1.0;
-            g = (t < 0.25) ? 0.0 : ((t < 0.75) ? (t - 0.25) * 2.0 : 1.0);
-            b = (t < 0.5) ? 0.0 : (t - 0.5) * 2.0;
-            const double br = 0.2 + 0.8 * (t * t);
-            r *= br;
-            g *= br;
-            b *= br;
-            if (sc.flags & BHRT_FLAG_DOPPLER) {  // raytracer.c:233-294
-                // sin, cos of atan2(hy, hx) as hy / rxy, hx / rxy (rxy > 0: a disk hit lies at
-                // rxy >= disk_in), pow(dop, 4) as two squarings, dop / (1 / sqrt(f)) as
-                // dop * sqrt(f): each within a few ulp of the libm forms
-                double sp, cp;
-                if (rxy > 0.0) {
-                    const double ir = 1.0 / rxy;
-                    sp = hy * ir;
-                    cp = hx * ir;
-                } else {
-                    sincos(atan2(hy, hx), &sp, &cp);
-                }
-                const double dop = 1.0 + ((dx * -sp + dy * cp) + dz * 0.0) * 0.5;
-                const double z = dop * sqrt(1.0 - sc.rs / rxy);
-                if (z < 1.0) {
-                    b *= z;
-                    r = fmin(1.0, r * (2.0 - z));
-                } else {
-                    r *= 2.0 - z;
-                    b = fmin(1.0, b * z);
-                }
-                const double d2 = dop * dop, beam = d2 * d2;
-                r = clampd(r * beam, 0.0, 1.0);
-                g = clampd(g * beam, 0.0, 1.0);
-                b = clampd(b * beam, 0.0, 1.0);
-            }
-        } else if (res == RAY_HORIZON) {
-            r = g = b = 0.0;
-        } else {
-            const double t = 0.5 * (dy + 1.0);
-            r = (1.0 - t) * 1.0 + t * 0.5;
-            g = (1.0 - t) * 1.0 + t * 0.7;
-            b = (1.0 - t) * 1.0 + t * 1.0;
-        }
-        if (s.rgb_r) {
-            s.rgb_r[i] = r;
-            s.rgb_g[i] = g;
-            s.rgb_b[i] = b;
-        }
-        if (s.rgba32f || s.rgba8) {  // the display path (renderer.cpp:2090-2125)
-            const float fr = (float)r, fg = (float)g, fb = (float)b;
-            if (s.rgba32f) reinterpret_cast<float4*>(s.rgba32f)[i] = make_float4(fr, fg, fb, 1.0f);
-            if (s.rgba8)
-                reinterpret_cast<unsigned*>(s.rgba8)[i] =
-                    to_u8(fr) | (to_u8(fg) << 8) | (to_u8(fb) << 16) | (to_u8(1.0f) << 24);
-        }
+        colour_of(kp.sc, res, res == RAY_DISK ? s.hit_x[i] : 0.0,
+                  res == RAY_DISK ? s.hit_y[i] : 0.0, dx, dy, dz, r, g, b);
+        store_colour(s, i, r, g, b);
     }
 }
 
@@ -1351,7 +1410,7 @@ __global__ void k_path(const bhrt_kparams kp, double t0, double ox, double oy, d
     if (kp.sc.max_steps > 0) {
         for (;;) {
             const int k_before = R.k;
-            term = ray_iterate<METHOD, false, SPIN0, true, true>(R, kp.sc, n);
+            term = ray_iterate<METHOD, false, SPIN0, true, true>(R, kp.sc, n, hsel_of(kp.sc));
             // positions of the iterations executed (a fixed-point jump repeats p_k)
             for (int j = k_before; j < R.k && path && num >= 0 && num < max_positions; j++) {
                 path[num].x = R.px;
@@ -1495,7 +1554,7 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
         launch_trace_pair<METHOD, DISK, SPIN0, FAR, false>(kp, st);
     }
     if (ev1) (void)hipEventRecord(ev1, st);
-    if (kp.out.rgb_r || kp.out.rgba32f || kp.out.rgba8) {
+    if (!kp.colour_fused && (kp.out.rgb_r || kp.out.rgba32f || kp.out.rgba8)) {
         if (kp.src == BHRT_SRC_CAMERA)
             k_colour<BHRT_SRC_CAMERA><<<grid_for(reinterpret_cast<const void*>(&k_colour<BHRT_SRC_CAMERA>),
                                                  kp.n), 256, 0, st>>>(kp);

@@ -88,6 +88,50 @@ def compare(got, want, rtol, check_sky, what="", fields=None):
     return worst
 
 
+KNIFE_EDGE = 1e-9  # rays whose reference margin to a threshold is below this
+
+
+def full_frame_report(got, want, margin, check_sky, rtol=1e-5):
+    """Every-ray comparison of a GPU frame with the oracle's (integers exact, floats within
+    rtol, NaN pattern identical), with the oracle's knife-edge margin of each ray: a mismatch
+    on a ray whose margin is below KNIFE_EDGE is a listed knife-edge ray, any other is a
+    parity failure. Returns a JSON-able dict; report["unexplained"] must be 0."""
+    n = len(want["result"])
+    bad = np.zeros(n, dtype=bool)
+    rep = {"rays": int(n)}
+    for f in INT_FIELDS:
+        d = np.asarray(got[f]) != np.asarray(want[f])
+        rep[f + "_mismatch"] = int(d.sum())
+        bad |= d
+    worst = {}
+    for f in FLOAT_FIELDS + (SKY_FIELDS if check_sky else ()):
+        a, b = np.asarray(got[f]), np.asarray(want[f])
+        na, nb = np.isnan(a), np.isnan(b)
+        d = na != nb
+        ok = ~(na | nb)
+        rel = np.zeros(n)
+        rel[ok] = np.abs(a[ok] - b[ok]) / np.maximum(np.maximum(np.abs(a[ok]), np.abs(b[ok])),
+                                                     1e-300)
+        small = ok & (np.abs(a - b) <= 1e-9)  # (values at ~0: absolute floor, as in compare)
+        d |= (rel > rtol) & ~small
+        rep[f + "_violations"] = int(d.sum())
+        worst[f] = float(rel[ok & ~bad].max()) if (ok & ~bad).any() else 0.0
+        bad |= d
+    knife = margin < KNIFE_EDGE
+    rep["max_rel_err_on_matching_rays"] = worst
+    rep["mismatched_rays"] = int(bad.sum())
+    rep["knife_edge_rays"] = int(knife.sum())
+    rep["mismatches_on_knife_edge"] = int((bad & knife).sum())
+    rep["unexplained"] = int((bad & ~knife).sum())
+    rep["unexplained_ids"] = np.nonzero(bad & ~knife)[0][:20].tolist()
+    rep["knife_edge_ids"] = np.nonzero(knife)[0][:200].tolist()
+    rep["min_margin"] = float(np.nanmin(margin)) if n else None
+    edges = [0, 1e-12, 1e-9, 1e-6, 1e-3, np.inf]
+    rep["margin_histogram"] = {f"[{lo:g},{hi:g})": int(((margin >= lo) & (margin < hi)).sum())
+                               for lo, hi in zip(edges, edges[1:])}
+    return rep
+
+
 def fixture_outputs(g):
     return {k[4:]: v for k, v in g.items() if k.startswith("out_")}
 

@@ -13,8 +13,8 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from conftest import (camera_from, compare, fixture_outputs, golden, golden_names, rays_from,
-                      scene_from, sky_pinned)
+from conftest import (camera_from, compare, fixture_outputs, full_frame_report, golden,
+                      golden_names, rays_from, scene_from, sky_pinned)
 from bhrt import abi, configs
 
 pytestmark = pytest.mark.gpu
@@ -565,6 +565,32 @@ def test_async_frames_in_flight_equal_sync_frames(bhrt_lib, monkeypatch, registe
                                      c.flags, fields=tuple(arrays))
         for f in arrays:
             assert np.array_equal(arrays[f], want[f], equal_nan=True), (cname, camname, f)
+
+
+@pytest.mark.parametrize("cname", ["C1", "C2"])
+def test_full_frame_every_ray_vs_oracle(bhrt_lib, oracle, cname):
+    """Every ray of the BASELINE frame (C1 256x256, C2 1920x1080, camera B) against the
+    oracle: classes and steps exact, floats within 1e-5, NaN pattern; a mismatch is allowed
+    only on a listed knife-edge ray (oracle margin to a threshold < 1e-9).
+    C3-C5 get the same comparison from tools/full_frame_parity.py (profiles/)."""
+    import torch
+    c = configs.CONFIGS[cname]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera("B")
+    W, H = c.width, c.height
+    t = {f: torch.zeros(W * H, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
+                        device="cuda") for f in abi.SOA_FIELDS}
+    bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                 bhrt_lib.soa_from_tensors(t), 0)
+    torch.cuda.synchronize()
+    got = {f: v.cpu().numpy() for f, v in t.items()}
+    want, margin = oracle.render_frame_margin(bh, dk, cfg, cam, W, H, c.method, c.flags,
+                                              threads=16)
+    rep = full_frame_report(got, want, margin, sky_pinned(c.method))
+    print(cname, {k: rep[k] for k in ("rays", "mismatched_rays", "knife_edge_rays",
+                                      "min_margin", "max_rel_err_on_matching_rays")})
+    assert rep["unexplained"] == 0, rep
+    assert rep["rays"] == W * H
 
 
 def test_registered_frames_with_freed_arrays_and_pageable_copies(bhrt_lib, monkeypatch):

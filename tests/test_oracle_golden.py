@@ -201,3 +201,31 @@ def test_numpy_camera_rays_match_the_oracle(oracle):
                 O.orc_camera_ray_direction(x, y, 0.5, 0.5, W, H, C.byref(cam), C.byref(d))
                 got = rays["direction"][y * W + x]
                 assert np.allclose(got, (d.x, d.y, d.z), rtol=0, atol=1e-15), (name, x, y)
+
+
+def test_knife_edge_margins(oracle):
+    """orc_render_frame_margin (the knife-edge list of tools/full_frame_parity.py and the
+    full-frame GPU tests): outputs identical to orc_render_frame for every config, margins
+    positive, and a ray put exactly on a threshold gets margin 0 -- here max_ray_distance set
+    to the distance a MAX_DISTANCE ray reaches at its exit iteration."""
+    from bhrt import abi, configs
+    cam = configs.camera("B")
+    for name in ("C1", "C2", "C3", "C4", "C5"):
+        c = configs.CONFIGS[name]
+        bh, dk, cfg = c.scene()
+        a = oracle.render_frame(bh, dk, cfg, cam, 40, 24, c.method, c.flags, threads=4)
+        b, m = oracle.render_frame_margin(bh, dk, cfg, cam, 40, 24, c.method, c.flags,
+                                          threads=4)
+        for f in a:
+            assert np.array_equal(a[f], b[f], equal_nan=True), (name, f)
+        assert np.all(m > 0) and np.all(np.isfinite(m)), name
+    c = configs.CONFIGS["C4"]
+    bh, dk, cfg = c.scene()
+    f, m = oracle.render_frame_margin(bh, None, cfg, cam, 40, 24, c.method, 0, threads=4)
+    i = int(np.nonzero(f["result"] == abi.RAY_MAX_DISTANCE)[0][0])
+    assert m[i] > 1e-9
+    # a distance threshold exactly at the (k-1)-th partial sum is hit by rounding only: put
+    # it at the distance this ray reports and the exit decision is taken at margin 0
+    cfg.max_ray_distance = float(f["distance"][i])
+    f2, m2 = oracle.render_frame_margin(bh, None, cfg, cam, 40, 24, c.method, 0, threads=4)
+    assert f2["result"][i] == abi.RAY_MAX_DISTANCE and m2[i] == 0.0

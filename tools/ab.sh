@@ -1,13 +1,18 @@
 #!/bin/bash
-# A/B of libbhrt build variants on the bench workload (two interleaved rounds).
+# A/B of libbhrt build variants on the bench workload (interleaved rounds). A variant is
+# NAME (raytracing-engine-in-c_amd/ab/libbhrt_NAME.so; "base" = the in-tree library) or
+# NAME:VAR=VALUE (the same library with one environment variable set, e.g.
+# fc:BHRT_FUSE_COLOUR=0).
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/ab; mkdir -p $OUT
 CFG=${CFG:-C2}
-VARIANTS=${VARIANTS:-"base w4 fs fsw4 w5 ctr"}
+VARIANTS=${VARIANTS:-"base"}
 for round in $(seq 1 ${ROUNDS:-2}); do
   for v in $VARIANTS; do
-    if [ "$v" = base ]; then lib=raytracing-engine-in-c_amd/libbhrt.so; else lib=raytracing-engine-in-c_amd/ab/libbhrt_$v.so; fi
-    BHRT_LIB=$lib timeout -k 10 300 python bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline $EXTRA > $OUT/${v}_$round.json 2>$OUT/${v}_$round.err || { echo "$v failed"; tail -3 $OUT/${v}_$round.err; exit 1; }
-    python3 -c "import json,sys; d=json.load(open('$OUT/${v}_$round.json')); print('$v', $round, d['value'], d['kernel']['avg_ms'])"
+    name=${v%%:*}; envset=""; [ "$name" != "$v" ] && envset=${v#*:}
+    if [ "$name" = base ]; then lib=raytracing-engine-in-c_amd/libbhrt.so; else lib=raytracing-engine-in-c_amd/ab/libbhrt_$name.so; fi
+    tag=$(echo "$v" | tr ':=' '__')
+    env $envset BHRT_LIB=$lib timeout -k 10 300 python bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline $EXTRA > $OUT/${CFG}_${tag}_$round.json 2>$OUT/${CFG}_${tag}_$round.err || { echo "$v failed"; tail -3 $OUT/${CFG}_${tag}_$round.err; exit 1; }
+    python3 -c "import json,sys; d=json.load(open('$OUT/${CFG}_${tag}_$round.json')); print('$CFG', '$v', $round, d['value'], d['kernel']['avg_ms'])"
   done
 done

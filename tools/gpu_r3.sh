@@ -19,7 +19,7 @@ if [ -z "$SKIP_BENCH" ]; then
     || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
   cat $OUT/bench.json
 fi
-for n in ${REHEARSE_N:-2 4}; do
+[ -n "$SKIP_REHEARSE" ] || for n in ${REHEARSE_N:-2 4}; do
   for c in ${REHEARSE_CFGS:-C2 C5}; do
     echo "== rehearsal --gpus $n --config $c"
     BHRT_BENCH_SHARE_DEVICE=1 timeout -k 10 400 python bench.py --gpus $n --config $c --steps 4 --warmup 1 \
@@ -29,3 +29,22 @@ for n in ${REHEARSE_N:-2 4}; do
   done
 done
 echo done
+# optional same-box A/B of kernel variants (ab/libbhrt_<v>.so) against REF, with the full-frame
+# bit-exact comparison first (tools/ab_bitexact.sh)
+if [ -n "$AB_VARIANTS" ]; then
+  for v in $AB_VARIANTS; do
+    echo "== bitexact $v vs $AB_REF"
+    cp raytracing-engine-in-c_amd/libbhrt.so /tmp/libbhrt_intree.so
+    cp raytracing-engine-in-c_amd/ab/libbhrt_$v.so raytracing-engine-in-c_amd/libbhrt.so
+    REF=$AB_REF CONFIGS="${AB_CFGS:-C2 C3 C4 C5}" bash tools/ab_bitexact.sh > $OUT/bitexact_$v.txt 2>&1
+    rc=$?
+    cp /tmp/libbhrt_intree.so raytracing-engine-in-c_amd/libbhrt.so
+    cat $OUT/bitexact_$v.txt
+    [ $rc -eq 0 ] || { echo "bitexact failed"; exit 1; }
+  done
+  for c in ${AB_CFGS:-C2 C3 C4 C5}; do
+    echo "== ab $c"
+    CFG=$c VARIANTS="$AB_REF $AB_VARIANTS" ROUNDS=${AB_ROUNDS:-2} EXTRA="--no-host-path" bash tools/ab.sh || exit 1
+  done
+fi
+echo all-done
