@@ -616,7 +616,7 @@ def test_registered_frames_with_freed_arrays_and_pageable_copies(bhrt_lib, monke
                                      bhrt_lib.soa_from_tensors(t), 0)
         torch.cuda.synchronize()
         refs.append({f: v.cpu().numpy() for f, v in t.items()})
-    src = torch.arange(1 << 18, dtype=torch.float64, device="cuda")
+    src = torch.arange(1 << 20, dtype=torch.float64, device="cuda")
     for it in range(6):
         junk = [np.full(777 + 13 * k, k, dtype=np.uint8) for k in range(64)]  # heap neighbours
         sets = []
