@@ -483,6 +483,12 @@ static void fill_camera(bhrt_kparams* kp, const bhrt_camera* cam, int W, int H) 
     k->p0[1] = p0.y;
     k->p0[2] = p0.z;
     k->use_approx = r > kp->sc.rs_x15;
+    /* the carried sin/cos of the origin's state angles start from the
+     * reference's own libm values: state[2..3] = (th0, ph0) are st, ct, sp, cp above, and
+     * state[1] = r0 is read as an angle by ray_derivatives */
+    k->sp = sp;
+    k->s_r0 = sin(r);
+    k->c_r0 = cos(r);
 }
 
 /* one timed trace-kernel launch on `stream` (the context's own if NULL) */

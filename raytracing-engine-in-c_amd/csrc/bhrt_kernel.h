@@ -21,8 +21,10 @@ extern "C" {
 enum { BHRT_SRC_RAYS = 0, BHRT_SRC_CAMERA = 1 };
 enum { BHRT_NUM_COUNTERS = 5 }; /* rays, iterations, stages full/far/kerr */
 enum { BHRT_MAX_QUEUE_BITS = 5, BHRT_QUEUE_STRIDE_MAX = 64 }; /* ray queues of k_trace */
-enum { BHRT_INIT_FIELDS = 21 }; /* y0..y5, y6, y7, dx, dy, dz, px, py, pz, far_ok,
-                                   sin/cos of y1, y2, y3 */
+enum { BHRT_INIT_FIELDS = 21 }; /* ray arrays: y0..y5, y6, y7, dx, dy, dz, px, py, pz,
+                                   far_ok, sin/cos of y1, y2, y3; camera frames use the first
+                                   BHRT_INIT_FIELDS_CAMERA rows (the rest is the shared origin) */
+enum { BHRT_INIT_FIELDS_CAMERA = 8 }; /* y4, y5, y6, y7, dx, dy, dz, far_ok */
 
 typedef struct {
     /* scene constants (raytracer.c:65-130, 465, 556-571, 652-659; spacetime.c:22) */
@@ -53,6 +55,8 @@ typedef struct {
     double st_cp, st_sp, ct, ct_cp, ct_sp, st, neg_sp, cp, r_st; /* trig products */
     double g_tt, g_rr, g_hh;         /* calculate_schwarzschild_metric(r0)      */
     double p0[3];                    /* spherical_to_cartesian(r0, th0, ph0)    */
+    double sp;                       /* sin(ph0)                                */
+    double s_r0, c_r0;               /* sin, cos(r0): state[1] as ray_derivatives' theta */
     int use_approx;                  /* r0 > 15 rs                              */
     int st_tiny;                     /* fabs(sin th0) < BH_EPSILON              */
 } bhrt_camera_k;

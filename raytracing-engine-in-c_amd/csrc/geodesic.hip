@@ -938,9 +938,40 @@ __device__ __forceinline__ void store_hit(const bhrt_frame_soa& s, int i, const 
     if (s.sky_z) s.sky_z[i] = sz;
 }
 
+// A ray's initial state from the k_init table. A camera frame's table holds only what differs
+// between its rays (BHRT_INIT_FIELDS_CAMERA rows: 64 B per ray instead of 168); the shared
+// origin -- state[0..3], its Cartesian point and the sin/cos of its angles -- comes from the
+// launch's camera block (wave-uniform).
 __device__ __forceinline__ void load_init(const bhrt_kparams& kp, int i, Ray_& R) {
     const double* f = kp.init;
     const long n = kp.n;
+    if (kp.src == BHRT_SRC_CAMERA) {
+        const bhrt_camera_k& cm = kp.cam;
+        R.y[0] = 0.0;
+        R.y[1] = cm.r0;
+        R.y[2] = cm.th0;
+        R.y[3] = cm.ph0;
+        R.y[4] = f[i];
+        R.y[5] = f[n + i];
+        R.y6 = f[2 * n + i];
+        R.y7 = f[3 * n + i];
+        R.dx = f[4 * n + i];
+        R.dy = f[5 * n + i];
+        R.dz = f[6 * n + i];
+        R.far_ok = f[7 * n + i] != 0.0;
+        R.px = cm.p0[0];
+        R.py = cm.p0[1];
+        R.pz = cm.p0[2];
+        R.s1 = cm.s_r0;
+        R.c1 = cm.c_r0;
+        R.s2 = cm.st;
+        R.c2 = cm.ct;
+        R.s3 = cm.sp;
+        R.c3 = cm.cp;
+        R.dist = 0.0;
+        R.k = 0;
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 6; j++) R.y[j] = f[j * n + i];
     R.y6 = f[6 * n + i];
@@ -1081,40 +1112,49 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
     return s;
 }
 
-// Per-ray set-up pass (integrate_photon_path's prologue, raytracer.c:355-507) into the
-// [BHRT_INIT_FIELDS][n] state table the trace kernel refills from. Kept out of the
+// Per-ray set-up pass (integrate_photon_path's prologue, raytracer.c:355-507) into the state
+// table the trace kernel refills from ([BHRT_INIT_FIELDS][n] for ray arrays; for a camera frame
+// only the BHRT_INIT_FIELDS_CAMERA rows that differ between rays, 64 B per ray). Kept out of the
 // persistent loop so that neither the camera uniforms nor acos/atan2 occupy registers there.
 template <int SRC>
 __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
+    double* f = kp.init;
+    const long n = kp.n;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += gridDim.x * blockDim.x) {
         Ray_ R;
-        if (SRC == BHRT_SRC_CAMERA) {
+        if constexpr (SRC == BHRT_SRC_CAMERA) {  // the per-ray part only (load_init)
             ray_init_camera(R, kp.cam, i);
+            f[i] = R.y[4];
+            f[n + i] = R.y[5];
+            f[2 * n + i] = R.y6;
+            f[3 * n + i] = R.y7;
+            f[4 * n + i] = R.dx;
+            f[5 * n + i] = R.dy;
+            f[6 * n + i] = R.dz;
+            f[7 * n + i] = R.far_ok ? 1.0 : 0.0;
         } else {
             const Ray ray = kp.rays[i];
             ray_init_general(R, 0.0, ray.origin.x, ray.origin.y, ray.origin.z, ray.direction.x,
                              ray.direction.y, ray.direction.z, kp.sc);
-        }
-        double* f = kp.init;
-        const long n = kp.n;
 #pragma unroll
-        for (int j = 0; j < 6; j++) f[j * n + i] = R.y[j];
-        f[6 * n + i] = R.y6;
-        f[7 * n + i] = R.y7;
-        f[8 * n + i] = R.dx;
-        f[9 * n + i] = R.dy;
-        f[10 * n + i] = R.dz;
-        f[11 * n + i] = R.px;
-        f[12 * n + i] = R.py;
-        f[13 * n + i] = R.pz;
-        f[14 * n + i] = R.far_ok ? 1.0 : 0.0;
-        trig_anchor(R);
-        f[15 * n + i] = R.s1;
-        f[16 * n + i] = R.c1;
-        f[17 * n + i] = R.s2;
-        f[18 * n + i] = R.c2;
-        f[19 * n + i] = R.s3;
-        f[20 * n + i] = R.c3;
+            for (int j = 0; j < 6; j++) f[j * n + i] = R.y[j];
+            f[6 * n + i] = R.y6;
+            f[7 * n + i] = R.y7;
+            f[8 * n + i] = R.dx;
+            f[9 * n + i] = R.dy;
+            f[10 * n + i] = R.dz;
+            f[11 * n + i] = R.px;
+            f[12 * n + i] = R.py;
+            f[13 * n + i] = R.pz;
+            f[14 * n + i] = R.far_ok ? 1.0 : 0.0;
+            trig_anchor(R);
+            f[15 * n + i] = R.s1;
+            f[16 * n + i] = R.c1;
+            f[17 * n + i] = R.s2;
+            f[18 * n + i] = R.c2;
+            f[19 * n + i] = R.s3;
+            f[20 * n + i] = R.c3;
+        }
     }
 }
 
@@ -1172,13 +1212,9 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const unsigned long long total =
         HUGE ? *(volatile unsigned long long*)(kp.ctl + 6) : (unsigned long long)kp.n;
     if (total == 0) return;
-    double as1 = 0.0, ac1 = 0.0, as2 = 0.0, ac2 = 0.0, as3 = 0.0, ac3 = 0.0;
-    if (INL) {  // trig_anchor of the origin state (r0, th0, ph0); the host keeps |r0| < 2^20
-        Counters dummy;
-        bhrt_sincos(kp.cam.r0, &as1, &ac1, &dummy);
-        bhrt_sincos(kp.cam.th0, &as2, &ac2, &dummy);
-        bhrt_sincos(kp.cam.ph0, &as3, &ac3, &dummy);
-    }
+    // sin, cos of the origin state's angles (r0, th0, ph0): the host's libm values
+    const double as1 = kp.cam.s_r0, ac1 = kp.cam.c_r0, as2 = kp.cam.st, ac2 = kp.cam.ct,
+                 as3 = kp.cam.sp, ac3 = kp.cam.cp;
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
     Counters n;
