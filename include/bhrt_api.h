@@ -332,6 +332,11 @@ int bhrt_device_count(void);
  * (1..64; 0 = per scene: 8 for RK4 at spin 0, else 64). Affects speed only. */
 void bhrt_set_refill_threshold(int lanes);
 
+/* Tuning knob: the order in which the next device camera frames of n rays claim their rays --
+ * d_order, a device array holding a permutation of [0, n) (this thread; NULL or n = 0: ray id
+ * order). Results are the same in any order; only the schedule changes. */
+void bhrt_set_claim_order(const int* d_order, int n);
+
 /* update_particles (particle_sim.c:505-566) applied `steps` times in one device round trip:
  * the particle array is copied to the GPU once, stepped `steps` times by the HIP kernel and
  * copied back (steps == 1 is exactly update_particles). Returns 0, or -1 on invalid

@@ -59,6 +59,7 @@ _PROTOS = {
     "bhrt_get_stats": (C.c_int, [_P(abi.Stats), C.c_int]),
     "bhrt_device_count": (C.c_int, []),
     "bhrt_set_refill_threshold": (None, [C.c_int]),
+    "bhrt_set_claim_order": (None, [C.c_void_p, C.c_int]),
     "bhrt_last_error": (C.c_char_p, []),
     "bh_initialize": (C.c_void_p, []),
     "bh_shutdown": (None, [C.c_void_p]),
@@ -161,6 +162,12 @@ def render_frame_device(bh, dk, cfg, cam, width, height, rows, method, flags, so
                                            height, _ptr(rows), method, flags, C.byref(soa),
                                            C.c_void_p(stream) if stream else None),
            "bhrt_render_frame_device")
+
+
+def set_claim_order(d_order_ptr, n):
+    """bhrt_set_claim_order: the claim order (device int32 permutation of [0, n)) of this
+    thread's next device camera frames of n rays; None / 0 = ray id order."""
+    load().bhrt_set_claim_order(d_order_ptr, int(n))
 
 
 def shard_rows(height, rows):

@@ -154,6 +154,13 @@ static _Thread_local devctx_t* g_ctx[BHRT_MAX_DEV];
 static _Thread_local bhrt_stats g_stats;
 static int g_refill = 0; /* 0: chosen per scene (refill_default) */
 
+static __thread const int* g_order;
+static __thread int g_order_n;
+void bhrt_set_claim_order(const int* d_order, int n) {
+    g_order = n > 0 ? d_order : NULL;
+    g_order_n = d_order ? n : 0;
+}
+
 void bhrt_set_refill_threshold(int lanes) {
     g_refill = lanes <= 0 ? 0 : (lanes > 64 ? 64 : lanes);
 }
@@ -162,7 +169,10 @@ void bhrt_set_refill_threshold(int lanes) {
  * spread over 1..max_steps iterations (C2), so idle lanes are refilled early (8). Otherwise
  * (Kerr: straight-line stages; RKF45: fixed point after a few attempts) rays are short-lived
  * and similar, each refill is an HBM-latency stall, and a wave refills only once drained. */
+static int env_int(const char* name, int dflt);
 static int refill_default(const bhrt_scene_k* s) {
+    const int r = env_int("BHRT_REFILL", 0); /* A/B override */
+    if (r >= 1 && r <= 64) return r;
     return (s->method == INTEGRATOR_RK4 && s->spin0) ? 8 : 64;
 }
 
@@ -596,6 +606,7 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
     kp.n = nrows * W;
     kp.init = (double*)scratch;
     kp.out = *out;
+    if (g_order && g_order_n == kp.n) kp.order = g_order;
     return launch(c, &kp, (hipStream_t)stream);
 }
 

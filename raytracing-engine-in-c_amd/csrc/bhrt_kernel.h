@@ -91,6 +91,8 @@ typedef struct {
                              remainder >> claim_shift, 2^claim_shift >= waves * claim_div / queues */
     int colour_fused;     /* the trace kernel writes the colour outputs (rgb, rgba32f, rgba8)
                              of each ray at its exit; else a separate colour pass runs */
+    const int* order;     /* camera frames: the claim order, queue position -> ray id (a
+                             permutation of [0, n)); NULL = ray id order */
 } bhrt_kparams;
 
 /* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and

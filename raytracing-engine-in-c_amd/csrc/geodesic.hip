@@ -1123,7 +1123,8 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += gridDim.x * blockDim.x) {
         Ray_ R;
         if constexpr (SRC == BHRT_SRC_CAMERA) {  // the per-ray part only (load_init)
-            ray_init_camera(R, kp.cam, i);
+            // row i of the table is the i-th ray of the claim order
+            ray_init_camera(R, kp.cam, kp.order ? kp.order[i] : i);
             f[i] = R.y[4];
             f[n + i] = R.y[5];
             f[2 * n + i] = R.y6;
@@ -1329,8 +1330,10 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             }
             if (!live) {
                 if (ok) {
-                    rid = HUGE ? kp.redo[id] : (int)id;
-                    if (INL) {
+                    // queue position -> ray id; the k_init table is in queue order
+                    const int qpos = (int)id;
+                    rid = HUGE ? kp.redo[id] : (kp.order ? kp.order[qpos] : qpos);
+                    if (INL || (HUGE && kp.order)) {  // (the redo list holds ray ids)
                         ray_init_camera(R, kp.cam, rid);
                         R.s1 = as1;
                         R.c1 = ac1;
@@ -1339,7 +1342,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                         R.s3 = as3;
                         R.c3 = ac3;
                     } else {
-                        load_init(kp, rid, R);
+                        load_init(kp, HUGE ? rid : qpos, R);
                     }
                     // the first iteration's state recovery (the loop is skipped at max_steps <= 0);
                     // an in-kernel camera set-up has a finite origin (|r0| < 2^20, host-checked),
