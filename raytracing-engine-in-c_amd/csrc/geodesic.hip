@@ -175,6 +175,17 @@ __device__ __forceinline__ bool sincos_shift_wide(double a, double s0, double c0
     return true;
 }
 
+// sin(delta) and cos(delta) - 1 for |delta| <= 1/16: shift_or_eval's polynomials
+__device__ __forceinline__ void rotation_coeffs(double delta, double& sd, double& cm1) {
+    constexpr double S1 = -0.16666666666662605, S2 = 0.00833333327878775,
+                     S3 = -0.00019839069723619096;
+    constexpr double C1 = 0.04166666666666157, C2 = -0.0013888888827212717,
+                     C3 = 2.479927034006378e-05;
+    const double z = delta * delta;
+    sd = delta + (z * delta) * fmac_k(z, fmac_k(z, S3, S2), S1);
+    cm1 = z * __builtin_fma(z, fmac_k(z, fmac_k(z, C3, C2), C1), -0.5);
+}
+
 // sin, cos of x given those of a nearby a, as the trace loop needs them: every RK stage after
 // the first evaluates ray_derivatives at theta = y1 + delta (the stage increment; |delta| < 0.09
 // on a full C2 frame), and the three angles of the state move by one step per iteration.
@@ -367,6 +378,21 @@ template <int METHOD, bool SPIN0, bool FAR, bool HUGE>
 constexpr bool hoist_sums() {
     return METHOD == INTEGRATOR_RKF45 && zero_accel<SPIN0, FAR>() &&
            repair_at_refill<METHOD, FAR, HUGE>();
+}
+
+// On the same zero-acceleration paths state[2] (theta of the position) advances by a per-ray
+// constant times h -- h * (the step's weighted sum of the constant state[5]) -- so within a
+// step-size regime the angle turns by the same nominal increment delta every iteration. Its
+// sin and cos then follow by a fixed rotation: sin(delta) and cos(delta) - 1 are formed once
+// per regime (when h changes, at most three times per ray), and each iteration is the two
+// FMA pairs of the shift alone instead of forming delta's polynomials again. The rotation
+// tracks the nominal angle, which differs from the rounded state by the states' rounding
+// (<= 1 ulp of theta per iteration); the per-iteration shift it replaces carries its own
+// rounding the same way.
+template <int METHOD, bool SPIN0, bool FAR, bool HUGE>
+constexpr bool rotation_trig() {
+    return zero_accel<SPIN0, FAR>() && repair_at_refill<METHOD, FAR, HUGE>() &&
+           (METHOD == INTEGRATOR_RK4 || METHOD == INTEGRATOR_RKF45);
 }
 
 // The step's stage sums (math_util.c:162-207, 367-391), one expression each so that the
@@ -606,6 +632,8 @@ struct Ray_ {
     double dist;
     double s1, c1, s2, c2, s3, c3;  // sin, cos of y[1], y[2], y[3] (carried)
     double zs[6];       // per-ray stage sums of components 0..2 (hoist_sums)
+    double cd_h, cd_sd, cd_cm1;  // rotation_trig: the step size the rotation is for (NaN:
+                                 // none), sin(delta) and cos(delta) - 1 of its increment
     int k;              // iterations executed
     bool far_ok;        // use_analytic_approx && impact_parameter > 0
 };
@@ -787,12 +815,19 @@ struct HSel {  // the four step sizes of the schedule, hoisted out of the kernel
 // selected by v_cndmask. Left visible as loads, the select chain over them became ONE load at a
 // selected address, and the promoted step-size array an LDS table: a ds_read_b64 and an
 // lgkmcnt wait at the head of every iteration's dependency chain.
+template <bool V>
 __device__ __forceinline__ double opaque(double x) {
-    asm volatile("" : "+s"(x));
+    if (V)
+        asm volatile("" : "+v"(x));
+    else
+        asm volatile("" : "+s"(x));
     return x;
 }
+// V: the step sizes in VGPRs (8 more registers; each select is then one v_cndmask per half
+// instead of a v_mov from the SGPR and a v_cndmask): where the loop has registers to spare
+template <bool V = false>
 __device__ __forceinline__ HSel hsel_of(const Scene& sc) {
-    return HSel{opaque(sc.h_far), opaque(sc.h_15), opaque(sc.h_5), opaque(sc.h_2_5)};
+    return HSel{opaque<V>(sc.h_far), opaque<V>(sc.h_15), opaque<V>(sc.h_5), opaque<V>(sc.h_2_5)};
 }
 
 // :543-548, state NaN/Inf recovery at the top of an iteration. One test of the sum
@@ -844,7 +879,36 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
         // (a != 0, accelerations 0) never reads them, and the compiler keeps a dead
         // loop-carried advance alive otherwise (C5: 45 instructions of the loop)
         if (SPIN0) trig_advance(tr.a, R.y[1], R.s1, R.c1, hc);
-        trig_advance(a2, R.y[2], R.s2, R.c2, hc);
+        if constexpr (rotation_trig<METHOD, SPIN0, FAR, HUGE>()) {
+            if (__builtin_expect(!(h == R.cd_h), 0)) {  // a new regime (or none cached)
+                // the nominal increment of state[2]: h/6 * ((v + 2v) + 2v) + v (rk4_step) or
+                // h * sum5 (rkf45_attempt), v = state[5]
+                double d;
+                if (METHOD == INTEGRATOR_RK4) {
+                    double a = R.y[5];
+                    a = rk4_acc(a, R.y[5]);
+                    a = rk4_acc(a, R.y[5]);
+                    d = (h * (1.0 / 6.0)) * (a + R.y[5]);
+                } else {
+                    d = h * R.zs[5];
+                }
+                if (fabs(d) <= 0.0625) {
+                    rotation_coeffs(d, R.cd_sd, R.cd_cm1);
+                    R.cd_h = h;
+                } else {
+                    R.cd_h = __builtin_nan("");
+                }
+            }
+            if (R.cd_h == h) {
+                const double s0 = R.s2, c0 = R.c2;
+                R.s2 = __builtin_fma(c0, R.cd_sd, __builtin_fma(s0, R.cd_cm1, s0));
+                R.c2 = __builtin_fma(-s0, R.cd_sd, __builtin_fma(c0, R.cd_cm1, c0));
+            } else {
+                trig_advance(a2, R.y[2], R.s2, R.c2, hc);
+            }
+        } else {
+            trig_advance(a2, R.y[2], R.s2, R.c2, hc);
+        }
         // on the zero-acceleration Kerr paths state[3] never changes (zero_accel): its sin,
         // cos stay as they are
         if (!zero_accel<SPIN0, FAR>()) trig_advance(a3, R.y[3], R.s3, R.c3, hc);
@@ -870,10 +934,11 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     } else {
         // the exits as selects (the reference's order: disk, horizon, distance, fixed point,
         // step budget; a disk hit overrides the others below)
-        int term = (R.y[1] <= sc.rs_x1_05) ? T_HORIZON
-                 : (R.dist >= sc.max_dist) ? T_MAXDIST
-                 : (R.k >= sc.max_steps)   ? T_MAXSTEPS
-                                           : T_NONE;
+        // (as three selects, lowest priority first: the nested form compiled to exec-mask
+        // branches)
+        int term = (R.k >= sc.max_steps) ? T_MAXSTEPS : T_NONE;
+        term = (R.dist >= sc.max_dist) ? T_MAXDIST : term;
+        term = (R.y[1] <= sc.rs_x1_05) ? T_HORIZON : term;
         // segment k = (p_k, p_{k-1}) is stored and scanned by trace_ray iff k < max_steps
         double qx, qy, qz;
         if (disk_hit(R, ox, oy, oz, sc, qx, qy, qz) & (R.k < sc.max_steps)) {
@@ -882,7 +947,7 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
             R.px = qx;
             R.py = qy;
             R.pz = qz;
-            R.dist += len3(qx - ox, qy - oy, qz - oz);
+            R.dist += seg_len(qx - ox, qy - oy, qz - oz);  // (= len3: sqrt_nr is sqrt here)
             term = T_DISK;
         }
         if (!moved && term == T_NONE) {
@@ -1093,6 +1158,21 @@ __device__ __forceinline__ void store_colour(const bhrt_frame_soa& s, int i, dou
 // (BHRT_COLOUR_IN_TRACE, bhrt_kernel.h; colour_fused) the colour outputs from the exit state in
 // registers. Other instantiations do not contain the colour code at all (its registers cost
 // more in the loop than the separate pass does).
+// The launch parameters as an opaque pointer into the kernel argument segment: the fields read
+// through it are loaded (scalar loads) where they are used, instead of being kept live across
+// the persistent loop. The refill's camera constants and the store's output pointers held that
+// way overflowed the 106 SGPRs into VGPR lanes (v_readlane in every block of the loop).
+#ifndef BHRT_COLD_KP
+#define BHRT_COLD_KP 1
+#endif
+typedef const __attribute__((address_space(4))) bhrt_kparams kparams_as4;
+// (k_trace's only argument: it starts the kernel argument segment)
+__device__ __forceinline__ const bhrt_kparams& cold(const bhrt_kparams&) {
+    kparams_as4* p = (kparams_as4*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const bhrt_kparams*)p;
+}
+
 template <int METHOD, bool DISK>
 __device__ __forceinline__ void store_ray(const bhrt_kparams& kp, int i, const Ray_& R, int term) {
     store_hit(kp.out, i, R, term, kp.sc);
@@ -1170,6 +1250,12 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 //    (profiles/r02_ab_v23_occupancy.txt).
 //  * C3 (RKF45 a = 0 disk) and C4 (RK4 Kerr disk) keep the compiler's choice: forcing one
 //    more wave spills in their hot blocks (-14%, -1.5%).
+// step sizes in VGPRs (hsel_of): C4's instantiation (RK4 Kerr with a disk, ~100 VGPRs)
+template <int METHOD, bool DISK, bool SPIN0>
+constexpr bool hsel_vgpr() {
+    return METHOD == INTEGRATOR_RK4 && DISK && !SPIN0;
+}
+
 template <int METHOD, bool DISK, bool SPIN0>
 constexpr int trace_waves() {
     return (METHOD == INTEGRATOR_RKF45 && !DISK && !SPIN0) ? 4
@@ -1252,9 +1338,12 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         s_q[wv][2] = (blockIdx.x * BHRT_TRACE_WAVES_PER_BLOCK + wv) & (nq - 1u);
         s_q[wv][3] = 0u;
     }
+    constexpr bool COLD = BHRT_COLD_KP;
     bool exhausted = false;  // no ids left to claim or hand out; wave-uniform
-    const HSel hsel = hsel_of(kp.sc);
+    const HSel hsel = hsel_of<hsel_vgpr<METHOD, DISK, SPIN0>()>(kp.sc);
     for (;;) {
+        // (re-laundered at the top of every trip, in wave-uniform control flow)
+        const bhrt_kparams& kc = COLD ? cold(kp) : kp;
         const unsigned long long live_mask = __ballot(live);
         int n_live = __popcll(live_mask);
         if (!exhausted && (64 - n_live >= kp.refill || n_live == 0)) {
@@ -1334,7 +1423,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     const int qpos = (int)id;
                     rid = HUGE ? kp.redo[id] : (kp.order ? kp.order[qpos] : qpos);
                     if (INL || (HUGE && kp.order)) {  // (the redo list holds ray ids)
-                        ray_init_camera(R, kp.cam, rid);
+                        ray_init_camera(R, kc.cam, rid);
                         R.s1 = as1;
                         R.c1 = ac1;
                         R.s2 = as2;
@@ -1350,10 +1439,11 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     if (repair_at_refill<METHOD, FAR, HUGE>() && kp.sc.max_steps > 0)
                         state_repair<!INL>(R, &n);
                     if (hoist_sums<METHOD, SPIN0, FAR, HUGE>()) zero_sums<METHOD>(R);
+                    if (rotation_trig<METHOD, SPIN0, FAR, HUGE>()) R.cd_h = __builtin_nan("");
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
-                        store_ray<METHOD, DISK>(kp, rid, R, T_MAXSTEPS);
+                        store_ray<METHOD, DISK>(kc, rid, R, T_MAXSTEPS);
                         live = false;
                     }
                 }
@@ -1381,7 +1471,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 kp.redo[atomicAdd(kp.ctl + 6, 1ull)] = rid;
                 live = false;
             } else if (term != T_NONE) {
-                store_ray<METHOD, DISK>(kp, rid, R, term);
+                store_ray<METHOD, DISK>(kc, rid, R, term);
                 live = false;
             }
         }

@@ -332,6 +332,40 @@ def test_refill_threshold_does_not_change_results(bhrt_lib, cname):
             assert np.array_equal(o[f], outs[0][f], equal_nan=True), f
 
 
+@pytest.mark.parametrize("cname", ["C2", "C3", "C4", "C5"])
+def test_claim_order_does_not_change_results(bhrt_lib, cname):
+    """bhrt_set_claim_order (the queue position -> ray id permutation of device camera frames)
+    is a speed knob only: a random permutation and the reversed order give the id order's
+    frame bit for bit, for the table (C2) and the in-kernel set-up (C3-C5) paths; a permutation
+    of another length is ignored."""
+    import torch
+    c = configs.CONFIGS[cname]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera("B")
+    W, H = 200, 120
+    n = W * H
+    g = torch.Generator().manual_seed(7)
+    orders = [None, torch.randperm(n, generator=g).to(torch.int32).cuda(),
+              torch.arange(n - 1, -1, -1, dtype=torch.int32, device="cuda"),
+              torch.arange(n + 64, dtype=torch.int32, device="cuda")]  # wrong length: ignored
+    outs = []
+    try:
+        for order in orders:
+            bhrt_lib.set_claim_order(order.data_ptr() if order is not None else None,
+                                     order.numel() if order is not None else 0)
+            t = {f: torch.full((n,), -1, dtype=torch.int32 if f in ("result", "steps")
+                               else torch.float64, device="cuda") for f in abi.SOA_FIELDS}
+            bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                         bhrt_lib.soa_from_tensors(t), 0)
+            torch.cuda.synchronize()
+            outs.append({f: v.cpu().numpy() for f, v in t.items()})
+    finally:
+        bhrt_lib.set_claim_order(None, 0)
+    for o in outs[1:]:
+        for f in abi.SOA_FIELDS:
+            assert np.array_equal(o[f], outs[0][f], equal_nan=True), f
+
+
 def test_empty_and_degenerate_inputs(bhrt_lib):
     bh, cfg = abi.black_hole(), abi.sim_config()
     r = bhrt_lib.trace_rays(np.zeros(0, dtype=abi.RAY_DTYPE), bh, None, cfg)
