@@ -289,9 +289,8 @@ int bhrt_render_frame(const BlackHoleParams* blackhole, const AccretionDiskParam
                       const bhrt_frame_soa* host_out);
 
 /* Asynchronous form of bhrt_render_frame: queues the frame and returns a ticket (> 0) in
- * *ticket; the host arrays receive the frame while the GPU traces (through pinned staging; with
- * BHRT_HOST_REGISTER=1, by DMA into the whole pages inside each array, page-locked for the
- * frame's flight) and must not be read or freed before bhrt_frame_wait(ticket) returns. Three
+ * *ticket; the host arrays receive the frame through libbhrt's pinned staging (caller memory
+ * is never page-locked) and must not be read or freed before bhrt_frame_wait(ticket) returns. Three
  * frames may be in flight per host thread; a fourth issue first completes the oldest frame,
  * whose own bhrt_frame_wait then returns its result (once). Each frame needs its own arrays. */
 int bhrt_render_frame_async(const BlackHoleParams* blackhole, const AccretionDiskParams* disk,

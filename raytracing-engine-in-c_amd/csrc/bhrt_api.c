@@ -133,7 +133,7 @@ typedef struct {
     hipStream_t stream2, copy;
     hipEvent_t chunk_done[BHRT_MAX_CHUNKS], chunk_copied[BHRT_MAX_CHUNKS];
     /* per frame slot of bhrt_render_frame_async: device SoA of every chunk, pinned staging
-     * (only when the caller's arrays cannot be registered), chunk traced / chunk copied */
+     * of the caller's fields, chunk traced / chunk copied */
     struct {
         void* d_soa;
         size_t cap_soa;
@@ -396,6 +396,28 @@ static double sqrt_upper_bound(double outer) {
     return s;
 }
 
+/* Whether every state the trace loop can reach from an initial state within 2^40 stays below
+ * 2^400 for max_steps steps with the far-field branch taking part (geodesic.hip
+ * repair_at_refill: the far-field instantiations then run the state recovery once per ray and
+ * the division-free RKF45 accept test). Stage accelerations are clamped to 10, zero, or -- in
+ * the far-field branch, only where y0 > 15 rs -- y5 * 2M / y0^2 with a factor below
+ * C = 2M / (15 rs)^2. With h the largest step size, S = 18 >= the largest stage weight sum of
+ * RK4 (1) and RKF45 (17.4), W = 1.5 >= the final combination's (RK4 1, RKF45 1.4) and q = h S C
+ * < 1/2, a stage velocity is at most 2 (V + 10 h S) for velocities V at the step's start, so
+ * V' <= g V + a with g = 1 + 2 h W C, a = 20 h W: V_N <= g^N (V_0 + N a); the position moves
+ * by at most 2 h W (V + 10 h S) per step. */
+static int far_bounded(const bhrt_scene_k* s) {
+    if (s->max_steps <= 0) return 1;
+    if (!(s->two_m >= 0.0) || !(s->rs_x15 > 0.0 || s->two_m == 0.0)) return 0;
+    const double C = s->two_m == 0.0 ? 0.0 : s->two_m / (s->rs_x15 * s->rs_x15) * (1.0 + 1e-9);
+    const double h = fmax(fmax(fabs(s->h_2_5), fabs(s->h_5)), fmax(fabs(s->h_15), fabs(s->h_far)));
+    const double S = 18.0, W = 1.5, N = (double)s->max_steps;
+    if (!isfinite(C) || !isfinite(h) || !(h * S * C < 0.5)) return 0;
+    const double logv = log2(0x1p40 + N * 20.0 * h * W) + N * log1p(2.0 * h * W * C) / log(2.0);
+    const double logp = log2(0x1p40 + N * 2.0 * h * W * (exp2(fmin(logv, 1000.0)) + 10.0 * h * S));
+    return logv <= 400.0 && logp <= 400.0;
+}
+
 static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const AccretionDiskParams* dk,
                       const SimulationConfig* cfg, IntegrationMethod method, int flags) {
     memset(kp, 0, sizeof *kp);
@@ -422,6 +444,7 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
     s->method = (int)method;
     s->flags = flags;
     s->spin0 = bh->spin == 0.0;
+    s->far_bounded = far_bounded(s);
     s->has_disk = dk != NULL;
     if (dk) {
         s->disk_in = dk->inner_radius;
@@ -791,22 +814,12 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
  * chunk's workgroups fill the CUs its predecessor's tail (the longest rays) frees. Each
  * finished chunk is copied on the copy stream into pinned staging while later chunks trace,
  * and un-permuted into the caller's arrays by OpenMP threads when the frame is waited for
- * (the next frames in flight keep the GPU busy meanwhile). Opt-in (BHRT_HOST_REGISTER=1): the
- * whole pages INSIDE each of the caller's arrays are page-locked while the GPU traces
- * (hipHostRegister) and each chunk is DMA'd straight into them, one 2-D copy per field
- * un-permuting the row blocks; the bytes of an array's partial first and last pages go
- * through staging. DESIGN.md §4 "Host-buffer frames". */
-#define BHRT_EDGE_STAGE ((size_t)BHRT_NFIELDS * 2 * 4096)
+ * (the next frames in flight keep the GPU busy meanwhile). The caller's arrays are never
+ * page-locked: libbhrt registers no caller memory (DESIGN.md §4 "Host-buffer frames" -- the
+ * round-3 removal of the registered path and why). */
 
 typedef struct {
-    size_t stage_off; /* in the device's pinned staging of the frame slot */
-    char* dst;        /* caller memory */
-    size_t bytes;
-    int dev;
-} edge_piece;
-
-typedef struct {
-    int active, ticket, ndev, K, shards, W, H, direct;
+    int active, ticket, ndev, K, shards, W, H;
     int reaped_ticket, reaped_rc; /* a frame a later issue waited for implicitly */
     unsigned long long last_use;
     int timing;             /* BHRT_HOST_TIMING: print where the frame's time went (device 0) */
@@ -816,126 +829,11 @@ typedef struct {
     shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
     bhrt_rows rows[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
     size_t stage_off[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
-    /* direct mode: [rlo, rhi) = the registered whole pages inside field f's array (0 = none) */
-    uintptr_t rlo[BHRT_NFIELDS], rhi[BHRT_NFIELDS];
-    edge_piece* pieces;     /* staged bytes outside [rlo, rhi), copied into place at wait */
-    int npieces, cap_pieces;
-    size_t edge_stage[BHRT_MAX_DEV];
 } host_frame;
 
 static _Thread_local host_frame* g_frames; /* [BHRT_FRAME_SLOTS], allocated on first use */
 static _Thread_local int g_next_ticket;
 static _Thread_local unsigned long long g_frame_clock;
-
-static void unregister_host(host_frame* f) {
-    for (int k = 0; k < BHRT_NFIELDS; k++)
-        if (f->rlo[k]) {
-            (void)hipHostUnregister((void*)f->rlo[k]);
-            f->rlo[k] = f->rhi[k] = 0;
-        }
-}
-
-/* Page-lock the whole pages inside each requested field's array: [round up(p), round down(p +
- * bytes)). Nothing outside the caller's arrays is ever registered, so no other allocation
- * can start inside a registered page (see DESIGN.md §4 for why that matters), and arrays of
- * different frames never share a registration. Any failure -- a range the caller (or anyone
- * else) registered already, an array shorter than two pages -- unregisters what this frame
- * registered and returns -1: the frame then stages. */
-static int register_host(host_frame* f) {
-    const uintptr_t pg = 4096;
-    for (int k = 0; k < BHRT_NFIELDS; k++) {
-        f->rlo[k] = f->rhi[k] = 0;
-        const uintptr_t p = (uintptr_t)*soa_slot(&f->host, k);
-        if (!p) continue;
-        const uintptr_t lo = (p + pg - 1) & ~(pg - 1),
-                        hi = (p + k_fsize[k] * (size_t)f->W * (size_t)f->H) & ~(pg - 1);
-        if (hi < lo + 2 * pg || hipHostRegister((void*)lo, hi - lo, hipHostRegisterPortable) !=
-                                    hipSuccess) {
-            (void)hipGetLastError();
-            unregister_host(f);
-            return -1;
-        }
-        f->rlo[k] = lo;
-        f->rhi[k] = hi;
-    }
-    return 0;
-}
-
-static int add_piece(host_frame* f, int dev, size_t stage_off, char* dst, size_t bytes) {
-    if (f->npieces == f->cap_pieces) {
-        const int cap = f->cap_pieces ? 2 * f->cap_pieces : 64;
-        edge_piece* p = (edge_piece*)realloc(f->pieces, (size_t)cap * sizeof *p);
-        if (!p) {
-            set_err("host allocation failed");
-            return -1;
-        }
-        f->pieces = p;
-        f->cap_pieces = cap;
-    }
-    f->pieces[f->npieces++] = (edge_piece){stage_off, dst, bytes, dev};
-    return 0;
-}
-
-/* D2H of the device bytes [src, src + n) that land at caller address dst: the part inside
- * the field's registered pages [rlo, rhi) by DMA, the parts outside (an array's partial first
- * and last pages) into the device's edge staging, placed at wait */
-static int copy_span(host_frame* f, int dev, int fld, char* dst, const char* src, size_t n,
-                     char* stage, hipStream_t st) {
-    const uintptr_t a = (uintptr_t)dst, b = a + n, lo = f->rlo[fld], hi = f->rhi[fld];
-    const uintptr_t ia = a > lo ? a : lo, ib = b < hi ? b : hi;
-    if (ia < ib)
-        HIP_TRY(hipMemcpyAsync((char*)ia, src + (ia - a), ib - ia, hipMemcpyDeviceToHost, st));
-    const uintptr_t out[2][2] = {{a, b < lo ? b : lo}, {a > hi ? a : hi, b}};
-    for (int i = 0; i < 2; i++) {
-        if (out[i][0] >= out[i][1]) continue;
-        const size_t m = out[i][1] - out[i][0], off = f->edge_stage[dev];
-        if (off + m > BHRT_EDGE_STAGE) { /* (cannot happen: < 2 pages per field) */
-            set_err("edge staging overflow");
-            return -1;
-        }
-        f->edge_stage[dev] += m;
-        HIP_TRY(hipMemcpyAsync(stage + off, src + (out[i][0] - a), m, hipMemcpyDeviceToHost, st));
-        if (add_piece(f, dev, off, (char*)out[i][0], m)) return -1;
-    }
-    return 0;
-}
-
-/* DMA a finished chunk's wanted fields into the caller arrays: local row block i of shard sh
- * is image block i*S + sh, so the blocks inside the registered pages are ONE 2-D copy per
- * field; the (at most few) blocks that reach into an array's partial first or last page, and a
- * partial last block, go through copy_span. */
-static int copy_chunk_direct(host_frame* f, int dev, const shard_job* j, const bhrt_rows* rows,
-                             char* stage, hipStream_t st) {
-    const int W = f->W;
-    for (int fld = 0; fld < BHRT_NFIELDS; fld++) {
-        if (!WANTED(j, &f->host, fld)) continue;
-        char* dst = (char*)*soa_slot(&f->host, fld);
-        const char* src = (const char*)*soa_slot((bhrt_frame_soa*)&j->dev, fld);
-        const size_t fs = k_fsize[fld];
-        if (!rows || rows->num_shards <= 1) {
-            if (copy_span(f, dev, fld, dst, src, fs * (size_t)j->n, stage, st)) return -1;
-            continue;
-        }
-        const size_t rowb = fs * (size_t)W, B = rows->row_block, S = rows->num_shards,
-                     sh = rows->shard, blk = B * rowb;
-        const size_t nrow = (size_t)j->n / W, nfull = nrow / B, rem = nrow % B;
-        /* full blocks whose destination lies inside [rlo, rhi): a contiguous run [i0, i1) */
-        size_t i0 = 0, i1;
-        while (i0 < nfull && (uintptr_t)(dst + (i0 * S + sh) * blk) < f->rlo[fld]) i0++;
-        i1 = i0;
-        while (i1 < nfull && (uintptr_t)(dst + (i1 * S + sh) * blk) + blk <= f->rhi[fld]) i1++;
-        if (i1 > i0)
-            HIP_TRY(hipMemcpy2DAsync(dst + (i0 * S + sh) * blk, S * blk, src + i0 * blk, blk, blk,
-                                     i1 - i0, hipMemcpyDeviceToHost, st));
-        for (size_t i = 0; i < nfull + (rem ? 1 : 0); i++) {
-            if (i >= i0 && i < i1) continue;
-            const size_t bytes = i < nfull ? blk : rem * rowb;
-            if (copy_span(f, dev, fld, dst + (i * S + sh) * blk, src + i * blk, bytes, stage, st))
-                return -1;
-        }
-    }
-    return 0;
-}
 
 /* Chunks per device: each chunk's copy overlaps the tracing of the next, so only the last
  * chunk's copy follows the trace; but a chunk of C2 is traced by a full-chip persistent grid,
@@ -951,7 +849,7 @@ static int frame_chunks(int ndev, int W, int H, int block) {
     return K;
 }
 
-/* wait for every copy a frame queued, then place its staged bytes and drop its page locks */
+/* wait for every copy a frame queued, then un-permute its staged chunks into the caller arrays */
 static int frame_complete(host_frame* f) {
     const int slot = (int)(f - g_frames);
     int rc = 0;
@@ -965,18 +863,10 @@ static int frame_complete(host_frame* f) {
                 rc = -1;
                 break;
             }
-            if (!f->direct)
-                readback_finish(&f->jobs[k][d], &f->host,
-                                (const char*)c->fr[slot].h_stage + f->stage_off[k][d], f->W,
-                                f->shards > 1 ? &f->rows[k][d] : NULL);
+            readback_finish(&f->jobs[k][d], &f->host,
+                            (const char*)c->fr[slot].h_stage + f->stage_off[k][d], f->W,
+                            f->shards > 1 ? &f->rows[k][d] : NULL);
         }
-    if (rc == 0 && f->direct)
-        for (int i = 0; i < f->npieces; i++) {
-            const edge_piece* p = &f->pieces[i];
-            memcpy(p->dst, (const char*)f->jobs[0][p->dev].c->fr[slot].h_stage + p->stage_off,
-                   p->bytes);
-        }
-    unregister_host(f);
     if (f->timing && rc == 0) {
         struct timespec tw1;
         clock_gettime(CLOCK_MONOTONIC, &tw1);
@@ -985,8 +875,8 @@ static int frame_complete(host_frame* f) {
             (void)hipEventElapsedTime(&tr[k], f->t_ev[0], f->t_ev[2 + 2 * k]);
             (void)hipEventElapsedTime(&cp[k], f->t_ev[0], f->t_ev[3 + 2 * k]);
         }
-        fprintf(stderr, "libbhrt frame %d (%s, K=%d): enqueue %.2f ms, register %.2f ms, copies "
-                "queued %.2f ms, wait %.2f ms |", f->ticket, f->direct ? "direct" : "staging", f->K,
+        fprintf(stderr, "libbhrt frame %d (K=%d): enqueue %.2f ms, staging %.2f ms, copies "
+                "queued %.2f ms, wait %.2f ms |", f->ticket, f->K,
                 f->t_host[0], f->t_host[1], f->t_host[2],
                 (tw1.tv_sec - tw0.tv_sec) * 1e3 + (tw1.tv_nsec - tw0.tv_nsec) * 1e-6);
         for (int k = 0; k < f->K; k++) fprintf(stderr, " chunk %d traced %.2f copied %.2f", k, tr[k], cp[k]);
@@ -1036,8 +926,8 @@ static host_frame* frame_slot(void) {
 }
 
 /* A frame whose issue failed part way: its launches and copies may still be queued on the
- * slot's buffers and the caller's pages, so drain every stream it used before the page locks
- * go and the caller sees the error (the caller may then free its arrays). */
+ * slot's device buffers and pinned staging, so drain every stream it used before the caller
+ * sees the error (a later issue may then reallocate the slot's buffers). */
 static void frame_abort(host_frame* f, int ndev) {
     char err[sizeof g_err];
     memcpy(err, g_err, sizeof err);
@@ -1048,7 +938,6 @@ static void frame_abort(host_frame* f, int ndev) {
         (void)hipStreamSynchronize(c->stream2);
         (void)hipStreamSynchronize(c->copy);
     }
-    unregister_host(f);
     f->active = 0;
     memcpy(g_err, err, sizeof err);
 }
@@ -1103,28 +992,12 @@ static int frame_enqueue(host_frame* f, const BlackHoleParams* bh, const Accreti
             if (f->timing && d == 0) HIP_TRY(hipEventRecord(f->t_ev[2 + 2 * k], st));
         }
     clock_gettime(CLOCK_MONOTONIC, &th[1]);
-    /* Opt-in (BHRT_HOST_REGISTER=1): while the GPU traces, page-lock the caller's arrays and
-     * DMA straight into them. It saves the last chunk's host copy of a synchronous frame (C2:
-     * 11.0-11.7 vs 12.3-12.9 ms) but is slower with frames in flight (10.3 vs 9.8 ms per
-     * frame), so staging is the default. Frames under 8 MB always stage. */
-    size_t frame_bytes = 0;
-    for (int k = 0; k < BHRT_NFIELDS; k++)
-        if (*soa_slot((bhrt_frame_soa*)host, k)) frame_bytes += k_fsize[k] * (size_t)W * (size_t)H;
-    const char* reg_env = getenv("BHRT_HOST_REGISTER");
-    f->direct = frame_bytes >= ((size_t)8 << 20) && reg_env && atoi(reg_env) > 0 &&
-                register_host(f) == 0;
-    f->npieces = 0;
-    for (int d = 0; d < ndev; d++) {
+    for (int d = 0; d < ndev; d++) { /* pinned staging: every chunk of device d */
         devctx_t* c = f->jobs[0][d].c;
         size_t host_bytes = 0;
-        if (f->direct) { /* edge staging: the bytes outside [rlo, rhi), < 2 pages per field */
-            host_bytes = BHRT_EDGE_STAGE;
-            f->edge_stage[d] = 0;
-        } else {
-            for (int k = 0; k < K; k++) {
-                f->stage_off[k][d] = host_bytes;
-                host_bytes += wanted_bytes(&f->jobs[k][d], host);
-            }
+        for (int k = 0; k < K; k++) {
+            f->stage_off[k][d] = host_bytes;
+            host_bytes += wanted_bytes(&f->jobs[k][d], host);
         }
         HIP_TRY(hipSetDevice(d));
         if (ensure(&c->fr[slot].h_stage, &c->fr[slot].cap_stage, host_bytes ? host_bytes : 64, 1))
@@ -1136,13 +1009,9 @@ static int frame_enqueue(host_frame* f, const BlackHoleParams* bh, const Accreti
             devctx_t* c = f->jobs[k][d].c;
             HIP_TRY(hipSetDevice(d));
             HIP_TRY(hipStreamWaitEvent(c->copy, c->fr[slot].done[k], 0));
-            const bhrt_rows* r = shards > 1 ? &f->rows[k][d] : NULL;
             if (f->jobs[k][d].n > 0 &&
-                (f->direct ? copy_chunk_direct(f, d, &f->jobs[k][d], r,
-                                               (char*)c->fr[slot].h_stage, c->copy)
-                           : readback_issue(&f->jobs[k][d], host,
-                                            (char*)c->fr[slot].h_stage + f->stage_off[k][d],
-                                            c->copy)))
+                readback_issue(&f->jobs[k][d], host, (char*)c->fr[slot].h_stage + f->stage_off[k][d],
+                               c->copy))
                 return -1;
             HIP_TRY(hipEventRecord(c->fr[slot].copied[k], c->copy));
             if (f->timing && d == 0) HIP_TRY(hipEventRecord(f->t_ev[3 + 2 * k], c->copy));
@@ -1183,7 +1052,6 @@ static int render_frame_issue(const BlackHoleParams* bh, const AccretionDiskPara
     f->W = W;
     f->H = H;
     f->host = *host;
-    f->direct = 0;
     f->timing = getenv("BHRT_HOST_TIMING") != NULL;
     if (frame_enqueue(f, bh, dk, cfg, cam, method, flags)) {
         frame_abort(f, ndev);

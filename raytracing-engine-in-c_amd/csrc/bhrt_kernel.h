@@ -39,6 +39,8 @@ typedef struct {
     int has_disk;
     int flags;   /* BHRT_FLAG_* */
     int spin0;   /* blackhole->spin == 0.0 */
+    int far_bounded; /* a state within 2^40 stays below 2^400 over max_steps steps, far-field
+                        branch included (bhrt_api.c far_bounded; geodesic.hip repair_at_refill) */
 } bhrt_scene_k;
 
 typedef struct {

@@ -258,10 +258,13 @@ __device__ __forceinline__ void accel_literal(const double (&y)[6], double (&d)[
     }
 }
 
-// :141-153 -- non-finite -> 0 for all six, then |d[3..5]| <= 10.
+// :141-153 -- non-finite -> 0 for all six, then |d[3..5]| <= 10. BOUNDED (k_trace's hot
+// instantiations, repair_at_refill): d[0..2] are the stage state's velocities, finite there, so
+// only d[3..5] are looked at -- and d[0..2] stay the very registers of the stage state (no copies)
+template <bool BOUNDED = false>
 __device__ __forceinline__ void repair_clamp(double (&d)[6]) {
 #pragma unroll
-    for (int i = 0; i < 6; i++)
+    for (int i = BOUNDED ? 3 : 0; i < 6; i++)
         if (!isfinite(d[i])) d[i] = 0.0;
 #pragma unroll
     for (int i = 3; i < 6; i++) d[i] = fmin(fmax(d[i], -10.0), 10.0);
@@ -269,8 +272,10 @@ __device__ __forceinline__ void repair_clamp(double (&d)[6]) {
 
 // ray_derivatives (raytracer.c:44-154) for one RK stage. y = (t, r, theta, phi, tdot, rdot)
 // of the caller, read -- as the reference does -- as (r, theta, phi, v_r, v_theta, v_phi).
-// Stage counters: only FAR instantiations count per stage (a lane's branch varies); otherwise
-// every stage takes the one branch of the instantiation and k_trace derives the count.
+// Stage counters: FAR instantiations count their far-field stages (a lane's branch varies);
+// every other stage takes the instantiation's one other branch, and k_trace derives that count
+// from the iterations (the HUGE redo, whose RKF45 attempts can stop after stage 1, counts
+// every stage).
 template <bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const Scene& sc,
                                     bool far_ok, Counters& n, Trig1& tr, bool first) {
@@ -292,7 +297,7 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         } else {
             shift_or_eval(tr.a, tr.s, tr.c, y[1], st, ct, HUGE ? nullptr : &n);
         }
-        if (FAR) n.full++;
+        if (FAR && HUGE) n.full++;
         // Fast form, straight-line: the same three accelerations with the divisions as one
         // reciprocal and the products regrouped -- d3 = -M/r^2 + r (v_th^2 + (sin th v_ph)^2),
         // d4 = -2 v_r v_th / r + (sin th v_ph)(cos th v_ph),
@@ -322,14 +327,14 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
                           (int)(fabs(st) >= 0.01);
         if (__builtin_expect(plain, 1)) return;
         accel_literal(y, d, sc, st, ct);
-        repair_clamp(d);
+        repair_clamp<!HUGE>(d);
         return;
     }
     // :131-138
     d[3] = 0.0;
     d[4] = 0.0;
     d[5] = 0.0;
-    if (FAR) n.kerr++;
+    if (FAR && HUGE) n.kerr++;
     // Far-field and Kerr stages: the repair / clamps never change a value here but run as the
     // reference's pass whenever a component is not a plain |d| <= 10 value (NaN and Inf fail
     // the test). d[0..2] = y[3..5] need no test: the iteration starts from a finite state, and
@@ -338,7 +343,7 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
     const int plain = (int)(fabs(d[3]) <= 10.0) & (int)(fabs(d[4]) <= 10.0) &
                       (int)(fabs(d[5]) <= 10.0);
     if (plain) return;
-    repair_clamp(d);
+    repair_clamp<!HUGE>(d);
 }
 
 // Where the loop-top state recovery (raytracer.c:543-548) can only ever act on the first
@@ -350,11 +355,17 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
 // -- and h times stage values of state[3..5] (bounded by the initial velocities, |v| < 2^512
 // for any finite set-up, plus 18 per step) to state[0..2], which cannot reach 2^1024 within
 // 2^31 steps. For the same reason RKF45's non-finite-k1 reject (math_util.c:318-333) can
-// never fire there. The far-field branch's 2M / r^2 is unclamped, so far-field instantiations
-// keep both checks every iteration (as does the HUGE redo).
+// never fire there.
+// The far-field branch's acceleration y5 * 2M / y0^2 is unclamped, but it only runs where
+// y0 > 15 rs, so its factor is below C = 2M / (15 rs)^2: per step the velocities grow by at
+// most a factor 1 + 2 h W C (plus 20 h W), W the step's largest weight sum. The host proves
+// from the scene (far_bounded, bhrt_api.c) that a state starting within 2^40 stays below 2^400
+// for max_steps steps; far-field instantiations then drop the checks too, and a ray whose
+// initial state exceeds 2^40 -- or every ray of a launch the host could not prove bounded --
+// is handed to the HUGE redo pass (k_trace's refill), which keeps both checks every iteration.
 template <int METHOD, bool FAR, bool HUGE>
 constexpr bool repair_at_refill() {
-    return (METHOD == INTEGRATOR_RK4 || METHOD == INTEGRATOR_RKF45) && !FAR && !HUGE;
+    return (METHOD == INTEGRATOR_RK4 || METHOD == INTEGRATOR_RKF45) && !HUGE;
 }
 
 // On the Kerr branch without the far-field one (a != 0, FAR = false) every stage's
@@ -842,6 +853,13 @@ __device__ __forceinline__ void state_repair(Ray_& R, Counters* hc) {
             if (!isfinite(R.y[i])) R.y[i] = (i < 4) ? 1.0 : 0.0;
         if (ANCHOR) trig_anchor(R, hc);
     }
+}
+
+// every component of the state within +-bound (NaN fails)
+__device__ __forceinline__ bool state_within(const Ray_& R, double bound) {
+    const double m = fmax(fmax(fmax(fabs(R.y[0]), fabs(R.y[1])), fmax(fabs(R.y[2]), fabs(R.y[3]))),
+                          fmax(fabs(R.y[4]), fabs(R.y[5])));
+    return m <= bound;
 }
 
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
@@ -1440,11 +1458,18 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                         state_repair<!INL>(R, &n);
                     if (hoist_sums<METHOD, SPIN0, FAR, HUGE>()) zero_sums<METHOD>(R);
                     if (rotation_trig<METHOD, SPIN0, FAR, HUGE>()) R.cd_h = __builtin_nan("");
+                    // the far-field bound (repair_at_refill) not proven for this ray: it is handed
+                    // to the HUGE redo pass after its first trip, like a large-argument ray (the
+                    // trip's one iteration is discarded; a branch here would cost spills at
+                    // every refill)
+                    if (FAR && !HUGE && !(kp.sc.far_bounded && state_within(R, 0x1p40)))
+                        n.huge = true;
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
                         store_ray<METHOD, DISK>(kc, rid, R, T_MAXSTEPS);
                         live = false;
+                        n.huge = false;
                     }
                 }
             }
@@ -1479,12 +1504,13 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const unsigned long long s0 = wave_sum(n.rays), s1 = wave_sum(n.iters),
                              s3 = wave_sum(n.far_);
     unsigned long long s2, s4;
-    if (FAR) {  // stages counted one by one
+    if (FAR && HUGE) {  // stages counted one by one
         s2 = wave_sum(n.full);
         s4 = wave_sum(n.kerr);
-    } else {    // every stage took the instantiation's branch
+    } else {  // every stage that was not a far-field one took the instantiation's branch
         const unsigned long long st =
-            s1 * (METHOD == INTEGRATOR_RK4 ? 4ull : (METHOD == INTEGRATOR_RKF45 ? 6ull : 0ull));
+            s1 * (METHOD == INTEGRATOR_RK4 ? 4ull : (METHOD == INTEGRATOR_RKF45 ? 6ull : 0ull)) -
+            (FAR ? s3 : 0ull);
         s2 = SPIN0 ? st : 0ull;
         s4 = SPIN0 ? 0ull : st;
     }
@@ -1647,7 +1673,8 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     // rays evicted by the large-argument check (normally none: every wave exits at once). 64
     // workgroups: the evicted rays are rare, and a full-chip grid of waves that only read the
     // count and exit costs ~15 us per frame (C3 +8.5% same-box, profiles/r02_ab_v24.txt)
-    int redo_blocks = blocks < 64 ? blocks : 64;
+    // A far-field launch the host could not prove bounded hands every ray over: full grid.
+    int redo_blocks = (FAR && !kp.sc.far_bounded) ? blocks : (blocks < 64 ? blocks : 64);
     if (redo_blocks > cap_huge) redo_blocks = cap_huge;
     k.claim_shift = claim_shift(redo_blocks, kp.claim_div, 0);  // (the redo list is one queue)
     k_trace<METHOD, DISK, SPIN0, FAR, true, INL><<<redo_blocks, 256, 0, st>>>(k);

@@ -6,7 +6,7 @@
  * operation runs synchronously at enqueue time (a valid schedule of stream order). Checks
  * that catch host-layer bugs: an operation on a stream of another device than the current
  * one, a device pointer of device A used on device B, a D2H copy into host memory that is
- * neither registered, nor pinned, nor a synchronous hipMemcpy, a double registration.
+ * neither pinned nor a synchronous hipMemcpy, any page-locking of caller memory.
  * Violations abort with a message (the test then fails). Test infrastructure only. */
 #define _GNU_SOURCE
 #include <hip/hip_runtime_api.h>
@@ -176,11 +176,14 @@ hipError_t hipHostFree(void* p) {
     free(p);
     return hipSuccess;
 }
+/* libbhrt page-locks no caller memory since round 3: any registration
+ * is a host-layer bug */
 hipError_t hipHostRegister(void* p, size_t n, unsigned flags) {
     (void)flags;
     if (((uintptr_t)p & 4095) || (n & 4095)) FAIL("hipHostRegister of an unaligned range");
     if (!inside_caller_array((uintptr_t)p, n))
         FAIL("hipHostRegister of [%p, +%zu): pages outside the caller's arrays", p, n);
+    FAIL("hipHostRegister of [%p, +%zu): libbhrt must not page-lock caller memory", p, n);
     if (overlaps_registration((uintptr_t)p, n)) return ret(hipErrorHostMemoryAlreadyRegistered);
     track(p, n, -2);
     return hipSuccess;

@@ -449,6 +449,29 @@ def test_large_argument_rays_take_the_redo_path(bhrt_lib, oracle):
         assert st["rays_redone"] > 0, st
 
 
+@pytest.mark.parametrize("method", [abi.INTEGRATOR_RK4, abi.INTEGRATOR_RKF45])
+def test_unbounded_far_field_launch_takes_the_redo_path(bhrt_lib, oracle, method):
+    """geodesic.hip repair_at_refill: the far-field instantiations drop the per-iteration state
+    recovery (and RKF45's literal accept quotient) only where bhrt_api.c far_bounded proves that
+    no state can overflow. A tiny black hole (M = 1e-3: the far-field factor 2M / (15 rs)^2 is
+    2.2, so h S C > 1/2) is not provable: every ray is handed to the HUGE redo pass, whose
+    literal per-iteration checks must give the oracle's frame (camera B origin beyond 15 rs,
+    so the frame runs the FAR instantiations). A normal scene hands over none."""
+    cam = configs.camera("B")
+    dk = abi.disk(0.006, 0.04, 1.0, 1.0)
+    W, H = 40, 24
+    for mass, expect_all in ((1.0e-3, True), (1.0, False)):
+        bh = abi.black_hole(mass, 0.0)
+        cfg = abi.sim_config(0.1, 100.0, 300, 1e-6)
+        bhrt_lib.stats(reset=True)
+        got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, method, 0)
+        st = bhrt_lib.stats(reset=True)
+        want = oracle.render_frame(bh, dk, cfg, cam, W, H, method, 0)
+        compare(got, want, RTOL, method != abi.INTEGRATOR_RK4, f"far-field M={mass}")
+        assert st["rays"] == W * H, st
+        assert st["rays_redone"] == (W * H if expect_all else 0), st
+
+
 def _display_u8(v):
     """(unsigned char)(std::min(1.0f, v) * 255.0f), renderer.cpp:2113-2116, on x86."""
     v = v.astype(np.float32)
@@ -500,13 +523,11 @@ def test_sub_pixel_offset_frames(bhrt_lib, oracle):
         compare(got, want, RTOL, False, f"sample {k}")
 
 
-@pytest.mark.parametrize("register", ["", "1"])
-def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch, register):
+def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch):
     """bhrt_render_frame traces a host-buffer frame in pipelined chunks (cyclic row-block
-    shards, copies overlapped with tracing); any chunk count gives the device frame, whether
-    the chunks are staged and un-permuted on the host (default) or DMA'd into the registered
-    caller arrays by 2-D copies (BHRT_HOST_REGISTER=1; 416 rows = 52 row blocks: uneven
-    shards, partial last blocks)."""
+    shards, copies overlapped with tracing, staged and un-permuted on the host); any chunk
+    count gives the device frame (416 rows = 52 row blocks: uneven shards, partial last
+    blocks)."""
     import torch
     c = configs.CONFIGS["C2"]
     bh, dk, cfg = c.scene()
@@ -518,9 +539,6 @@ def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch, register):
                                  bhrt_lib.soa_from_tensors(t), 0)
     torch.cuda.synchronize()
     ref = {f: v.cpu().numpy() for f, v in t.items()}
-    monkeypatch.setenv("BHRT_HOST_REGISTER", register)
-    if not register:
-        monkeypatch.delenv("BHRT_HOST_REGISTER")
     for chunks in ("1", "3", "4", "8"):
         monkeypatch.setenv("BHRT_HOST_CHUNKS", chunks)
         got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
@@ -530,7 +548,7 @@ def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch, register):
 
 def _frame_soa_in_one_buffer(n, fields, offset=0):
     """Caller arrays carved back to back out of ONE host allocation (fields share pages, and
-    the first starts `offset` bytes into a page): the registration must merge page ranges."""
+    the first starts `offset` bytes into a page)."""
     sizes = [n * (16 if f == "rgba32f" else 4 if f in ("result", "steps", "rgba8") else 8)
              for f in fields]
     buf = np.zeros(sum(sizes) + offset + 64, dtype=np.uint8)
@@ -544,21 +562,13 @@ def _frame_soa_in_one_buffer(n, fields, offset=0):
     return buf, arrays, soa
 
 
-@pytest.mark.parametrize("register", ["", "1"])
-def test_async_frames_in_flight_equal_sync_frames(bhrt_lib, monkeypatch, register):
+def test_async_frames_in_flight_equal_sync_frames(bhrt_lib):
     """bhrt_render_frame_async: four frames of different scenes queued back to back (three in
     flight, the fourth waits for the oldest slot), into separate host arrays -- one set
-    carved out of a single allocation at an odd page offset, one set page-locked by the
-    caller beforehand (hipHostRegister: used as it is, left registered) -- each equals the
-    synchronous frame; waiting twice, or for a ticket never issued, is an error. Staged
-    (default) and DMA'd into the page-locked arrays (BHRT_HOST_REGISTER=1)."""
-    if register:
-        monkeypatch.setenv("BHRT_HOST_REGISTER", register)
+    carved out of a single allocation at an odd page offset -- each equals the synchronous
+    frame; waiting twice, or for a ticket never issued, is an error."""
     L = bhrt_lib.load()
-    hip = C.CDLL("libamdhip64.so")
-    hip.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
-    hip.hipHostUnregister.argtypes = [C.c_void_p]
-    W, H = 1024, 576  # 590 k rays, 56 MB of fields: the DMA path, 2 chunks
+    W, H = 1024, 576  # 590 k rays, 56 MB of fields, 2 chunks
     jobs = [("C2", "B"), ("C4", "B"), ("C3", "A"), ("C2", "V")]
     outs, keep = [], []
     for i, (cname, camname) in enumerate(jobs):
@@ -569,29 +579,24 @@ def test_async_frames_in_flight_equal_sync_frames(bhrt_lib, monkeypatch, registe
         else:
             arrays, soa = abi.alloc_soa(W * H, fields)
         outs.append((arrays, soa))
-    pre = outs[3][0]["distance"]
-    assert hip.hipHostRegister(pre.ctypes.data, pre.nbytes, 0) == 0
-    try:
-        tickets = []
-        for (cname, camname), (arrays, soa) in zip(jobs, outs):
-            c = configs.CONFIGS[cname]
-            bh, dk, cfg = c.scene()
-            t = C.c_int(0)
-            assert L.bhrt_render_frame_async(C.byref(bh), C.byref(dk) if dk else None,
-                                             C.byref(cfg), C.byref(configs.camera(camname)), W,
-                                             H, c.method, c.flags, C.byref(soa),
-                                             C.byref(t)) == 0, bhrt_lib.last_error()
-            tickets.append(t.value)
-        assert len(set(tickets)) == 4 and min(tickets) > 0
-        # the fourth issue took the oldest frame's slot and completed frame 1 first; frame
-        # 1's own wait still returns its result, once
-        for t in tickets:
-            assert L.bhrt_frame_wait(t) == 0, bhrt_lib.last_error()
-        assert L.bhrt_frame_wait(tickets[0]) == -1  # already waited for
-        assert L.bhrt_frame_wait(tickets[-1]) == -1
-        assert L.bhrt_frame_wait(max(tickets) + 100) == -1
-    finally:
-        assert hip.hipHostUnregister(pre.ctypes.data) == 0  # still the caller's registration
+    tickets = []
+    for (cname, camname), (arrays, soa) in zip(jobs, outs):
+        c = configs.CONFIGS[cname]
+        bh, dk, cfg = c.scene()
+        t = C.c_int(0)
+        assert L.bhrt_render_frame_async(C.byref(bh), C.byref(dk) if dk else None,
+                                         C.byref(cfg), C.byref(configs.camera(camname)), W,
+                                         H, c.method, c.flags, C.byref(soa),
+                                         C.byref(t)) == 0, bhrt_lib.last_error()
+        tickets.append(t.value)
+    assert len(set(tickets)) == 4 and min(tickets) > 0
+    # the fourth issue took the oldest frame's slot and completed frame 1 first; frame
+    # 1's own wait still returns its result, once
+    for t in tickets:
+        assert L.bhrt_frame_wait(t) == 0, bhrt_lib.last_error()
+    assert L.bhrt_frame_wait(tickets[0]) == -1  # already waited for
+    assert L.bhrt_frame_wait(tickets[-1]) == -1
+    assert L.bhrt_frame_wait(max(tickets) + 100) == -1
     for (cname, camname), (arrays, _) in zip(jobs, outs):
         c = configs.CONFIGS[cname]
         bh, dk, cfg = c.scene()
@@ -627,21 +632,20 @@ def test_full_frame_every_ray_vs_oracle(bhrt_lib, oracle, cname):
     assert rep["rays"] == W * H
 
 
-def test_registered_frames_with_freed_arrays_and_pageable_copies(bhrt_lib, monkeypatch):
-    """BHRT_HOST_REGISTER=1 as a render loop that reallocates uses it: every frame's caller
-    arrays are freed right after the frame (some carved out of one allocation at odd
-    offsets, some small enough to come from the heap next to other allocations), two frames
-    in flight, and after every frame pageable torch D2H copies and heap allocations that
-    re-use the freed memory. libbhrt page-locks only whole pages inside each array (DESIGN.md
-    section 4), so no other allocation can start in a locked page; every frame must equal the
-    device frame and every pageable copy its source."""
+def test_frames_with_freed_arrays_and_pageable_copies(bhrt_lib, monkeypatch):
+    """A render loop that reallocates: every frame's caller arrays are freed right after the
+    frame (some carved out of one allocation at odd offsets, some small enough to come from
+    the heap next to other allocations), two frames in flight, and after every frame pageable
+    torch D2H copies and heap allocations that re-use the freed memory. libbhrt never
+    page-locks caller memory (the registered path and its faults were
+    removed in round 3); every frame must equal the device frame and every pageable copy its
+    source."""
     import torch
-    monkeypatch.setenv("BHRT_HOST_REGISTER", "1")
     L = bhrt_lib.load()
     c = configs.CONFIGS["C2"]
     bh, dk, cfg = c.scene()
     cams = [configs.camera("B"), configs.camera("A")]
-    W, H = 768, 432  # 332 k rays, 32 MB of fields: the DMA path, 2 chunks
+    W, H = 768, 432  # 332 k rays, 32 MB of fields, 2 chunks
     refs = []
     for cam in cams:
         t = {f: torch.zeros(W * H, dtype=torch.int32 if f in ("result", "steps") else

@@ -2,11 +2,12 @@
 
 tests/fakehip/fake_hip.c stands in for the HIP runtime with host memory tagged by device and
 synchronous streams, and aborts on a cross-device stream, event, copy or launch buffer, or on
-an asynchronous D2H copy into host memory that is neither pinned nor registered.
+an asynchronous D2H copy into host memory that is not pinned, or on any page-locking of caller
+memory (libbhrt registers none).
 tests/fakehip/multidev_driver.c stubs the trace launcher (it checks every launch buffer
 against the current device and writes an encoding of each ray's image pixel) and drives,
-from two host threads at once, frames split over two devices and several chunks (DMA into
-registered caller arrays, staged, frames in flight) and ray batches split over the devices,
+from two host threads at once, frames split over two devices and several chunks (staged,
+frames in flight) and ray batches split over the devices,
 checking that every value lands at its pixel. Built twice: ASan+UBSan and TSan."""
 import os
 import shutil
@@ -44,12 +45,9 @@ def run(exe, **env):
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
-@pytest.mark.parametrize("register", ["", "1"])
-def test_two_simulated_devices_asan_ubsan(tmp_path, register):
+def test_two_simulated_devices_asan_ubsan(tmp_path):
     exe = build(tmp_path, "multidev_asan", "address,undefined", openmp=True)
     env = {"ASAN_OPTIONS": "detect_leaks=0", "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}
-    if register:
-        env["BHRT_HOST_REGISTER"] = "1"
     r = run(exe, **env)
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
 
@@ -59,5 +57,5 @@ def test_two_simulated_devices_tsan(tmp_path):
     """Two host threads through the same library: per-thread contexts must not race. Built
     without OpenMP (libgomp is not TSan-instrumented); the host copies then run serially."""
     exe = build(tmp_path, "multidev_tsan", "thread", openmp=False)
-    r = run(exe, TSAN_OPTIONS="halt_on_error=1", BHRT_HOST_REGISTER="1")
+    r = run(exe, TSAN_OPTIONS="halt_on_error=1")
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
