@@ -1268,10 +1268,14 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 //    (profiles/r02_ab_v23_occupancy.txt).
 //  * C3 (RKF45 a = 0 disk) and C4 (RK4 Kerr disk) keep the compiler's choice: forcing one
 //    more wave spills in their hot blocks (-14%, -1.5%).
-// step sizes in VGPRs (hsel_of): C4's instantiation (RK4 Kerr with a disk, ~100 VGPRs)
+// step sizes in VGPRs (hsel_of): the RK4 disk instantiations. C4 (Kerr, ~100 VGPRs) has the
+// room; C2 (a = 0, capped at 128) gives its rare-lane blocks a few more spills but its iteration
+// loses 7 v_mov_b32 (an SGPR operand of v_cndmask next to VCC exceeds gfx9's one constant-bus
+// read, so each select first copied its SGPR half into a VGPR): +1.4% / +2.5% on two boxes,
+// bit-identical (profiles/r03_ab/ab_v30a.txt, ab_v30b.txt)
 template <int METHOD, bool DISK, bool SPIN0>
 constexpr bool hsel_vgpr() {
-    return METHOD == INTEGRATOR_RK4 && DISK && !SPIN0;
+    return METHOD == INTEGRATOR_RK4 && DISK;
 }
 
 template <int METHOD, bool DISK, bool SPIN0>
