@@ -96,6 +96,7 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 #define BHRT_MAX_CHUNKS 8   /* host-buffer frames: pipelined chunks per device            */
 #define BHRT_SCRATCH_SLOTS 4
 #define BHRT_FRAME_SLOTS 3  /* host-buffer frames in flight per thread (bhrt_render_frame_async) */
+#define BHRT_COPY_PARTS 4   /* host-buffer frames: a chunk's D2H in parts, each un-permuted as it lands */
 #define BHRT_NFIELDS 15
 
 typedef struct {
@@ -140,6 +141,7 @@ typedef struct {
         void* h_stage;
         size_t cap_stage;
         hipEvent_t done[BHRT_MAX_CHUNKS], copied[BHRT_MAX_CHUNKS];
+        hipEvent_t part[BHRT_MAX_CHUNKS][BHRT_COPY_PARTS]; /* part p of chunk k landed */
     } fr[BHRT_FRAME_SLOTS];
     /* busy span of the trace kernels since the last stats reset: span_ref is recorded before
      * the first launch; [span_lo, span_hi] = earliest start / latest end relative to it (ms).
@@ -271,12 +273,14 @@ static devctx_t* ctx_get(int device) {
         }
     for (int f = 0; f < BHRT_FRAME_SLOTS; f++)
         for (int i = 0; i < BHRT_MAX_CHUNKS; i++)
-            if (hipEventCreateWithFlags(&c->fr[f].done[i], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&c->fr[f].copied[i], hipEventDisableTiming) != hipSuccess) {
-                set_err("hipEventCreate failed");
-                free(c);
-                return NULL;
-            }
+            for (int q = -2; q < BHRT_COPY_PARTS; q++)
+                if (hipEventCreateWithFlags(q == -2 ? &c->fr[f].done[i]
+                                            : q == -1 ? &c->fr[f].copied[i] : &c->fr[f].part[i][q],
+                                            hipEventDisableTiming) != hipSuccess) {
+                    set_err("hipEventCreate failed");
+                    free(c);
+                    return NULL;
+                }
     g_ctx[device] = c;
     return c;
 }
@@ -722,15 +726,29 @@ static size_t wanted_bytes(const shard_job* j, const bhrt_frame_soa* host) {
     return bytes;
 }
 
-/* enqueue the D2H of a shard's wanted fields into pinned `stage` on stream st */
-static int readback_issue(shard_job* j, const bhrt_frame_soa* host, char* stage, hipStream_t st) {
+/* enqueue the D2H of a shard's wanted fields into pinned `stage` on stream st. With `parts`
+ * events, the fields are cut into up to BHRT_COPY_PARTS consecutive groups of about equal bytes,
+ * part q's event is recorded once its copies are queued and part_end[q] = the field after it
+ * (*nparts = the parts used): the host can un-permute a part while the next one copies. */
+static int readback_issue(shard_job* j, const bhrt_frame_soa* host, char* stage, hipStream_t st,
+                          hipEvent_t* parts, unsigned char* part_end, int* nparts) {
+    const size_t total = wanted_bytes(j, host);
     size_t off = 0;
+    int q = 0, last = -1;
+    for (int f = 0; f < BHRT_NFIELDS; f++)
+        if (WANTED(j, host, f)) last = f;
     for (int f = 0; f < BHRT_NFIELDS; f++) {
         if (!WANTED(j, host, f)) continue;
         HIP_TRY(hipMemcpyAsync(stage + off, *soa_slot(&j->dev, f), k_fsize[f] * (size_t)j->n,
                                hipMemcpyDeviceToHost, st));
         off += k_fsize[f] * (size_t)j->n;
+        if (parts && (f == last || (q < BHRT_COPY_PARTS - 1 &&
+                                    off * BHRT_COPY_PARTS >= total * (size_t)(q + 1)))) {
+            HIP_TRY(hipEventRecord(parts[q], st));
+            part_end[q++] = (unsigned char)(f + 1);
+        }
     }
+    if (nparts) *nparts = q;
     return 0;
 }
 
@@ -754,7 +772,7 @@ static int host_threads(void) {
 }
 
 static void readback_finish(const shard_job* j, const bhrt_frame_soa* host, const char* stage,
-                            int W, const bhrt_rows* rows) {
+                            int W, const bhrt_rows* rows, int f_lo, int f_hi) {
     /* every wanted field of the chunk as pieces of <= 1 MB (one image row at a time when the
      * rows are permuted), all copied in ONE parallel loop: a C2 chunk is ~50 MB, and a single
      * thread moves pinned staging at ~16 GB/s, which made the copies, not the GPU, the bound of
@@ -770,10 +788,11 @@ static void readback_finish(const shard_job* j, const bhrt_frame_soa* host, cons
         off[f] = o;
         if (!WANTED(j, host, f)) continue;
         const size_t total = k_fsize[f] * (size_t)j->n;
+        o += total;
+        if (f < f_lo || f >= f_hi) continue; /* (its bytes still precede later fields in stage) */
         npieces[f] = permute ? j->n / W : (long)((total + piece - 1) / piece);
         total_pieces += npieces[f];
         bytes_all += total;
-        o += total;
     }
     const int big = bytes_all >= ((size_t)1 << 22);
 #pragma omp parallel for schedule(static) num_threads(nthreads) if (big)
@@ -802,9 +821,9 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
     HIP_TRY(hipSetDevice(c->device));
     const size_t bytes = wanted_bytes(j, host);
     if (ensure(&c->h_stage, &c->cap_stage, bytes ? bytes : 64, 1)) return -1;
-    if (readback_issue(j, host, (char*)c->h_stage, c->stream)) return -1;
+    if (readback_issue(j, host, (char*)c->h_stage, c->stream, NULL, NULL, NULL)) return -1;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    readback_finish(j, host, (const char*)c->h_stage, W, rows);
+    readback_finish(j, host, (const char*)c->h_stage, W, rows, 0, BHRT_NFIELDS);
     return 0;
 }
 
@@ -829,6 +848,8 @@ typedef struct {
     shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
     bhrt_rows rows[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
     size_t stage_off[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
+    int nparts[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];   /* readback_issue's parts of each chunk */
+    unsigned char part_end[BHRT_MAX_CHUNKS][BHRT_MAX_DEV][BHRT_COPY_PARTS];
 } host_frame;
 
 static _Thread_local host_frame* g_frames; /* [BHRT_FRAME_SLOTS], allocated on first use */
@@ -858,14 +879,28 @@ static int frame_complete(host_frame* f) {
     for (int k = 0; k < f->K && rc == 0; k++)
         for (int d = 0; d < f->ndev && rc == 0; d++) {
             devctx_t* c = f->jobs[k][d].c;
-            if (hipSetDevice(d) != hipSuccess || hipEventSynchronize(c->fr[slot].copied[k]) != hipSuccess) {
-                set_err("frame %d: waiting for chunk %d of device %d failed", f->ticket, k, d);
+            if (hipSetDevice(d) != hipSuccess) {
+                set_err("frame %d: hipSetDevice(%d) failed", f->ticket, d);
                 rc = -1;
                 break;
             }
-            readback_finish(&f->jobs[k][d], &f->host,
-                            (const char*)c->fr[slot].h_stage + f->stage_off[k][d], f->W,
-                            f->shards > 1 ? &f->rows[k][d] : NULL);
+            /* each part of the chunk is un-permuted as soon as it has landed, while the next
+             * part still copies (a synchronous frame's last chunk: copy and host copy overlap) */
+            const int np = f->jobs[k][d].n > 0 ? f->nparts[k][d] : 0;
+            for (int q = 0, lo = 0; q < np && rc == 0; lo = f->part_end[k][d][q++]) {
+                if (hipEventSynchronize(c->fr[slot].part[k][q]) != hipSuccess) {
+                    set_err("frame %d: waiting for chunk %d of device %d failed", f->ticket, k, d);
+                    rc = -1;
+                    break;
+                }
+                readback_finish(&f->jobs[k][d], &f->host,
+                                (const char*)c->fr[slot].h_stage + f->stage_off[k][d], f->W,
+                                f->shards > 1 ? &f->rows[k][d] : NULL, lo, f->part_end[k][d][q]);
+            }
+            if (rc == 0 && hipEventSynchronize(c->fr[slot].copied[k]) != hipSuccess) {
+                set_err("frame %d: waiting for chunk %d of device %d failed", f->ticket, k, d);
+                rc = -1;
+            }
         }
     if (f->timing && rc == 0) {
         struct timespec tw1;
@@ -1009,9 +1044,10 @@ static int frame_enqueue(host_frame* f, const BlackHoleParams* bh, const Accreti
             devctx_t* c = f->jobs[k][d].c;
             HIP_TRY(hipSetDevice(d));
             HIP_TRY(hipStreamWaitEvent(c->copy, c->fr[slot].done[k], 0));
+            f->nparts[k][d] = 0;
             if (f->jobs[k][d].n > 0 &&
                 readback_issue(&f->jobs[k][d], host, (char*)c->fr[slot].h_stage + f->stage_off[k][d],
-                               c->copy))
+                               c->copy, c->fr[slot].part[k], f->part_end[k][d], &f->nparts[k][d]))
                 return -1;
             HIP_TRY(hipEventRecord(c->fr[slot].copied[k], c->copy));
             if (f->timing && d == 0) HIP_TRY(hipEventRecord(f->t_ev[3 + 2 * k], c->copy));
