@@ -1686,15 +1686,15 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
 
 template <int METHOD, bool DISK, bool SPIN0, bool FAR>
 int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    // camera rays set up inside k_trace where rays are short-lived: scenes with a disk (most
-    // rays end on it within tens of iterations: C4 +6.6%, C3 +16.5%) except the a = 0 RK4 path
-    // (C2: lifetimes up to max_steps, refills rare; its hot blocks must fit the 4-wave 128-VGPR
-    // cap), and the Kerr RKF45 path without a disk (C5: 51 attempts per ray since v21's cheaper
-    // attempts, so k_init's 168-byte table -- 0.7 GB written and read per 8K shard -- outweighs
-    // the set-up: +1.5% same-box, profiles/r02_ab_v20_occupancy.txt; it lost 5% on round 1's
-    // 193-attempt slab, r01_ab_v10.txt).
-    constexpr bool CAN_INL = DISK ? !(METHOD == INTEGRATOR_RK4 && SPIN0)
-                                  : (METHOD == INTEGRATOR_RKF45 && !SPIN0);
+    // camera rays set up inside k_trace (no k_init table, no table load at refill): scenes with
+    // a disk (most rays end on it within tens of iterations: C4 +6.6%, C3 +16.5%; the a = 0 RK4
+    // path since v31, whose in-kernel set-up now fits the 4-wave 128-VGPR cap with spills only
+    // in rare-lane blocks: C2 +1.2% same-box, profiles/r03_ab/ab_c2inl.txt), and the Kerr RKF45
+    // path without a disk (C5: 51 attempts per ray since v21's cheaper attempts, so k_init's
+    // 168-byte table -- 0.7 GB written and read per 8K shard -- outweighs the set-up: +1.5%
+    // same-box, profiles/r02_ab_v20_occupancy.txt; it lost 5% on round 1's 193-attempt slab,
+    // r01_ab_v10.txt).
+    constexpr bool CAN_INL = DISK ? true : (METHOD == INTEGRATOR_RKF45 && !SPIN0);
     const bool inl = CAN_INL && kp.src == BHRT_SRC_CAMERA && fabs(kp.cam.r0) < 1048576.0;
     if (inl)
         ;

@@ -35,22 +35,4 @@ for c in ${TRACE_CFGS-C2 C3 C4 C5}; do
   cat $OUT/trace_span_$c.txt
 done
 echo all-done
-# optional same-box A/B of kernel variants (ab/libbhrt_<v>.so) against ab/libbhrt_$AB_REF.so: each
-# variant's full frames compared bit for bit with the reference build first (tools/ab_bitexact.sh)
-if [ -n "$AB_VARIANTS" ]; then
-  for v in $AB_VARIANTS; do
-    echo "== bitexact $v vs $AB_REF"
-    cp raytracing-engine-in-c_amd/libbhrt.so /tmp/libbhrt_intree.so
-    cp raytracing-engine-in-c_amd/ab/libbhrt_$v.so raytracing-engine-in-c_amd/libbhrt.so
-    REF=$AB_REF CONFIGS="${AB_BITEXACT_CFGS:-C1 C2 C3 C4 C5}" bash tools/ab_bitexact.sh > $OUT/bitexact_$v.txt 2>&1
-    rc=$?
-    cp /tmp/libbhrt_intree.so raytracing-engine-in-c_amd/libbhrt.so
-    cat $OUT/bitexact_$v.txt
-    [ $rc -eq 0 ] || { echo "bitexact failed"; exit 1; }
-  done
-  for c in ${AB_CFGS:-C2 C3}; do
-    echo "== ab $c"
-    CFG=$c VARIANTS="$AB_REF $AB_VARIANTS" ROUNDS=${AB_ROUNDS:-2} EXTRA="--no-host-path" bash tools/ab.sh || exit 1
-  done
-fi
-echo ab-done
+[ -z "$AB_VARIANTS" ] || bash tools/ab_session.sh || exit 1
