@@ -29,6 +29,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--config", default="C2")
     p.add_argument("--frames", type=int, default=10)
+    p.add_argument("--orders", default="id,longest_first,max_steps_first,reverse",
+                   help="comma list; also tileWxH (WxH pixel tiles, row-major tiles)")
     a = p.parse_args()
     torch.cuda.set_device(0)
     lib.load()
@@ -51,6 +53,13 @@ def main():
     torch.cuda.synchronize()
     ref = {f: t.clone() for f, t in fbs[0].views.items()}
     steps = ref["steps"].to(torch.int64)
+    def tiles(tw, th):
+        """pixel ids tile by tile (tw x th pixels, tiles row-major, pixels row-major within)"""
+        assert W % tw == 0 and H % th == 0, (W, H, tw, th)
+        ty, tx, py, px = torch.meshgrid(torch.arange(H // th), torch.arange(W // tw),
+                                        torch.arange(th), torch.arange(tw), indexing="ij")
+        return ((ty * th + py) * W + tx * tw + px).reshape(-1).to(torch.int32).to(dev)
+
     orders = {
         "id": None,
         "longest_first": torch.argsort(-steps, stable=True).to(torch.int32),
@@ -58,7 +67,12 @@ def main():
                                          stable=True).to(torch.int32),
         "reverse": torch.arange(n - 1, -1, -1, device=dev, dtype=torch.int32),
     }
-    for name, order in orders.items():
+    for name in a.orders.split(","):
+        if name.startswith("tile"):
+            tw, th = (int(v) for v in name[4:].split("x"))
+            order = tiles(tw, th)
+        else:
+            order = orders[name]
         lib.set_claim_order(order.data_ptr() if order is not None else None,
                             n if order is not None else 0)
         for fb in fbs:
