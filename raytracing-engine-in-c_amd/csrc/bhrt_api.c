@@ -602,6 +602,29 @@ static int colour_args_bad(const bhrt_frame_soa* out, int method, int has_disk) 
     return 0;
 }
 
+/* The claim order of a camera launch (geodesic.hip claim_ray): the shard's W x nrows pixels in
+ * 64-pixel tiles -- 8x8, else 16x4, else 32x2, the first that divides the shard -- so a
+ * wavefront traces a compact patch of the image whose rays live alike. RK4 scenes only: same-box
+ * A/B against ray id order (profiles/r03_ab/tiles_v32.txt) C4 -2.1% kernel time, C2 neutral
+ * resident but +1.4% synchronous / +1.8% rgba8 host frames (a lone frame's drain is shorter);
+ * RKF45 scenes keep id order (C3 +1.5% slower with tiles, C5 neutral). BHRT_TILES=0: ray id
+ * order (A/B). */
+static void claim_tiles(bhrt_camera_k* k, int W, int nrows) {
+    static const int shape[3][2] = {{3, 3}, {4, 2}, {5, 1}}; /* log2 of tile width, height */
+    k->tiles_per_row = 0;
+    if (env_int("BHRT_TILES", 1) == 0) return;
+    for (int i = 0; i < 3; i++) {
+        const int tw = 1 << shape[i][0], th = 1 << shape[i][1];
+        if (W % tw == 0 && nrows % th == 0) {
+            k->tile_w_log2 = shape[i][0];
+            k->tile_h_log2 = shape[i][1];
+            k->tiles_per_row = W / tw;
+            k->inv_tiles_per_row = 1.0 / (double)k->tiles_per_row;
+            return;
+        }
+    }
+}
+
 int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParams* dk,
                              const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
                              const bhrt_rows* rows, IntegrationMethod method, int flags,
@@ -634,6 +657,7 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
     kp.init = (double*)scratch;
     kp.out = *out;
     if (g_order && g_order_n == kp.n) kp.order = g_order;
+    else if (method == INTEGRATOR_RK4) claim_tiles(&kp.cam, W, nrows);
     return launch(c, &kp, (hipStream_t)stream);
 }
 

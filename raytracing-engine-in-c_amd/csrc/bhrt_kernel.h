@@ -61,6 +61,10 @@ typedef struct {
     double s_r0, c_r0;               /* sin, cos(r0): state[1] as ray_derivatives' theta */
     int use_approx;                  /* r0 > 15 rs                              */
     int st_tiny;                     /* fabs(sin th0) < BH_EPSILON              */
+    /* claim order: the shard's pixels in tiles of 2^tile_w_log2 x 2^tile_h_log2 = 64 pixels
+     * (one wavefront), tiles row-major; tiles_per_row == 0: ray id order */
+    int tile_w_log2, tile_h_log2, tiles_per_row;
+    double inv_tiles_per_row;        /* RN(1 / tiles_per_row)                   */
 } bhrt_camera_k;
 
 /* Whether the trace kernel writes a scene's colour outputs at each ray's exit (no separate

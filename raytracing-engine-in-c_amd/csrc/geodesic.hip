@@ -1210,6 +1210,24 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
     return s;
 }
 
+// Queue position -> ray id of a camera launch: the caller's permutation (bhrt_set_claim_order),
+// else the shard's pixels tile by tile -- 64-pixel tiles (8x8, 16x4 or 32x2, whichever divides
+// the shard; bhrt_api.c claim_tiles), so a wavefront's rays are a compact patch of the image with
+// alike lifetimes (its lanes drain together, and a frame's last rays are short tiles, not long
+// row segments: claim-order probe, profiles/r03_claim_order_tiles.txt) -- else id order. Which
+// lane traces a ray never changes its arithmetic, so the frame is bit-identical in every order.
+__device__ __forceinline__ int claim_ray(const bhrt_kparams& kp, int qpos) {
+    if (kp.order) return kp.order[qpos];
+    const bhrt_camera_k& cm = kp.cam;
+    if (cm.tiles_per_row == 0) return qpos;
+    const int t = qpos >> 6, w = qpos & 63;
+    const int trow = div_floor(t, cm.tiles_per_row, cm.inv_tiles_per_row);
+    const int tcol = t - trow * cm.tiles_per_row;
+    const int prow = (trow << cm.tile_h_log2) + (w >> cm.tile_w_log2);
+    const int pcol = (tcol << cm.tile_w_log2) + (w & ((1 << cm.tile_w_log2) - 1));
+    return prow * cm.width + pcol;
+}
+
 // Per-ray set-up pass (integrate_photon_path's prologue, raytracer.c:355-507) into the state
 // table the trace kernel refills from ([BHRT_INIT_FIELDS][n] for ray arrays; for a camera frame
 // only the BHRT_INIT_FIELDS_CAMERA rows that differ between rays, 64 B per ray). Kept out of the
@@ -1222,7 +1240,7 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
         Ray_ R;
         if constexpr (SRC == BHRT_SRC_CAMERA) {  // the per-ray part only (load_init)
             // row i of the table is the i-th ray of the claim order
-            ray_init_camera(R, kp.cam, kp.order ? kp.order[i] : i);
+            ray_init_camera(R, kp.cam, claim_ray(kp, i));
             f[i] = R.y[4];
             f[n + i] = R.y[5];
             f[2 * n + i] = R.y6;
@@ -1443,8 +1461,9 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 if (ok) {
                     // queue position -> ray id; the k_init table is in queue order
                     const int qpos = (int)id;
-                    rid = HUGE ? kp.redo[id] : (kp.order ? kp.order[qpos] : qpos);
-                    if (INL || (HUGE && kp.order)) {  // (the redo list holds ray ids)
+                    rid = HUGE ? kp.redo[id] : (kp.src == BHRT_SRC_CAMERA ? claim_ray(kc, qpos) : qpos);
+                    // (the redo list holds ray ids; the k_init table is in claim order)
+                    if (INL || (HUGE && (kp.order || kp.cam.tiles_per_row))) {
                         ray_init_camera(R, kc.cam, rid);
                         R.s1 = as1;
                         R.c1 = ac1;

@@ -332,12 +332,13 @@ def test_refill_threshold_does_not_change_results(bhrt_lib, cname):
             assert np.array_equal(o[f], outs[0][f], equal_nan=True), f
 
 
-@pytest.mark.parametrize("cname", ["C2", "C3", "C4", "C5"])
-def test_claim_order_does_not_change_results(bhrt_lib, cname):
+@pytest.mark.parametrize("cname", ["C1", "C2", "C3", "C4", "C5"])
+def test_claim_order_does_not_change_results(bhrt_lib, monkeypatch, cname):
     """bhrt_set_claim_order (the queue position -> ray id permutation of device camera frames)
-    is a speed knob only: a random permutation and the reversed order give the id order's
-    frame bit for bit, for the table (C2) and the in-kernel set-up (C3-C5) paths; a permutation
-    of another length is ignored."""
+    is a speed knob only: the default tiled order (64-pixel tiles, geodesic.hip claim_ray), ray
+    id order (BHRT_TILES=0), a random permutation and the reversed order give the same frame
+    bit for bit, on the in-kernel set-up paths (C2-C5) and the k_init table path (C1); a
+    permutation of another length is ignored."""
     import torch
     c = configs.CONFIGS[cname]
     bh, dk, cfg = c.scene()
@@ -348,9 +349,15 @@ def test_claim_order_does_not_change_results(bhrt_lib, cname):
     orders = [None, torch.randperm(n, generator=g).to(torch.int32).cuda(),
               torch.arange(n - 1, -1, -1, dtype=torch.int32, device="cuda"),
               torch.arange(n + 64, dtype=torch.int32, device="cuda")]  # wrong length: ignored
+    orders.insert(1, "ids")
     outs = []
     try:
         for order in orders:
+            if isinstance(order, str):  # ray id order instead of the default tiles
+                monkeypatch.setenv("BHRT_TILES", "0")
+                order = None
+            else:
+                monkeypatch.delenv("BHRT_TILES", raising=False)
             bhrt_lib.set_claim_order(order.data_ptr() if order is not None else None,
                                      order.numel() if order is not None else 0)
             t = {f: torch.full((n,), -1, dtype=torch.int32 if f in ("result", "steps")
