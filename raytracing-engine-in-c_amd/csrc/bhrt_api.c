@@ -442,6 +442,20 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
     s->h_5 = fmin(dt * 0.01, 0.1);
     s->h_15 = fmin(dt * 0.1, 0.1);
     s->h_far = fmin(dt, 0.1);
+    /* the r interval each step size holds on (geodesic.hip ray_iterate caches the size and its
+     * interval per ray): the chain picks h_2_5 for r < t3, else h_5 for r < t2, else h_15 for
+     * r < t1, else h_far -- for any order of the thresholds */
+    {
+        const double t1 = s->rs_x15, t2 = s->rs_x5, t3 = s->rs_x2_5;
+        s->h_lo[3] = -INFINITY;
+        s->h_hi[3] = t3;
+        s->h_lo[2] = t3;
+        s->h_hi[2] = t2;
+        s->h_lo[1] = fmax(t2, t3);
+        s->h_hi[1] = t1;
+        s->h_lo[0] = fmax(t1, fmax(t2, t3));
+        s->h_hi[0] = INFINITY;
+    }
     s->max_dist = cfg->max_ray_distance;
     s->tol = cfg->tolerance;
     s->max_steps = cfg->max_integration_steps;

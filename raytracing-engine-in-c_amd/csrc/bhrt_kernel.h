@@ -31,6 +31,9 @@ typedef struct {
     double M, rs, two_m;
     double rs_x1_5, rs_x1_05, rs_x2_5, rs_x5, rs_x15, rs_eps;
     double h_2_5, h_5, h_15, h_far;
+    /* the r interval of each step size of the schedule, [h_lo[k], h_hi[k]): k = 0 h_far,
+     * 1 h_15, 2 h_5, 3 h_2_5 (an empty interval for a size the select chain never picks) */
+    double h_lo[4], h_hi[4];
     double max_dist, tol;
     double disk_in, disk_out, disk_tscale;
     double disk_in_sq, disk_out_sq; /* exact s-bounds of inner <= RN(sqrt(s)) <= outer */

@@ -645,6 +645,7 @@ struct Ray_ {
     double zs[6];       // per-ray stage sums of components 0..2 (hoist_sums)
     double cd_h, cd_sd, cd_cm1;  // rotation_trig: the step size the rotation is for (NaN:
                                  // none), sin(delta) and cos(delta) - 1 of its increment
+    double h, h_lo, h_hi;        // hcache: the step size and the r interval it holds on
     int k;              // iterations executed
     bool far_ok;        // use_analytic_approx && impact_parameter > 0
 };
@@ -862,6 +863,16 @@ __device__ __forceinline__ bool state_within(const Ray_& R, double bound) {
     return m <= bound;
 }
 
+// Where the step size is kept per ray with its r interval (ray_iterate): the RK4 Kerr path
+// (C4), whose ~80-VALU iteration spent 9 on the select chain: -3.6% kernel time same-box,
+// bit-identical (profiles/r03_ab/hcache_v33.txt). Elsewhere it measured neutral (C2, C5 --
+// where the changed code also moved some hit points by ~1e-15) or -1.4% (C3), so the chain
+// stays; k_path and the HUGE redo always select.
+template <int METHOD, bool SPIN0, bool HUGE>
+constexpr bool hcache() {
+    return METHOD == INTEGRATOR_RK4 && !SPIN0 && !HUGE;
+}
+
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
 // on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
 // hs: the step sizes in registers (k_trace), or NULL to read them from the scene.
@@ -875,10 +886,28 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     // step schedule (:556-571), written as selects so the first true test wins; fmin(h, 0.1)
     // is folded into the values (host)
     const double r = R.y[1];
-    double h = hs.far_;
-    h = (r < sc.rs_x15) ? hs.r15 : h;
-    h = (r < sc.rs_x5) ? hs.r5 : h;
-    h = (r < sc.rs_x2_5) ? hs.r2_5 : h;
+    double h;
+    if constexpr (hcache<METHOD, SPIN0, HUGE>()) {
+        // the size is cached per ray with the r interval it holds on (Scene h_lo / h_hi): a ray
+        // changes regime at most three times, so each iteration is two compares instead of the
+        // three compares and three 64-bit selects of the chain (NaN r: always re-selected,
+        // giving the chain's h_far)
+        if (__builtin_expect(!(r >= R.h_lo && r < R.h_hi), 0)) {
+            int k = 0;
+            k = (r < sc.rs_x15) ? 1 : k;
+            k = (r < sc.rs_x5) ? 2 : k;
+            k = (r < sc.rs_x2_5) ? 3 : k;
+            R.h = k == 0 ? hs.far_ : (k == 1 ? hs.r15 : (k == 2 ? hs.r5 : hs.r2_5));
+            R.h_lo = sc.h_lo[k];
+            R.h_hi = sc.h_hi[k];
+        }
+        h = R.h;
+    } else {
+        h = hs.far_;
+        h = (r < sc.rs_x15) ? hs.r15 : h;
+        h = (r < sc.rs_x5) ? hs.r5 : h;
+        h = (r < sc.rs_x2_5) ? hs.r2_5 : h;
+    }
     bool moved = true;
     if (METHOD != INTEGRATOR_RK4) n.iters++;  // RK4: counted at termination (k_trace)
     Trig1 tr{R.y[1], R.s1, R.c1};
@@ -1481,6 +1510,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                         state_repair<!INL>(R, &n);
                     if (hoist_sums<METHOD, SPIN0, FAR, HUGE>()) zero_sums<METHOD>(R);
                     if (rotation_trig<METHOD, SPIN0, FAR, HUGE>()) R.cd_h = __builtin_nan("");
+                    if (hcache<METHOD, SPIN0, HUGE>()) R.h_lo = R.h_hi = __builtin_nan("");  // select on entry
                     // the far-field bound (repair_at_refill) not proven for this ray: it is handed
                     // to the HUGE redo pass after its first trip, like a large-argument ray (the
                     // trip's one iteration is discarded; a branch here would cost spills at
