@@ -126,6 +126,12 @@ def parse():
     p.add_argument("--shard", type=int, default=None,
                    help="tiles mode, N = 1: render shard K of the frame instead of shard 0 "
                         "(to time every shard of a node frame on one GPU)")
+    p.add_argument("--plan-gpus", type=int, default=None,
+                   help="N = 1 only: render a shard (--shard K, default 0) of the frame the "
+                        "N-GPU run renders (configs.Config.frame(N): C2 at 8 is the 5433x3056 "
+                        "frame in 8 shards, C4 the 3840x2160 image in 8, C5 its 8 shards), so "
+                        "every rank's work of an N-GPU run can be timed on one GPU "
+                        "(tools/plan_shards.sh)")
     p.add_argument("--gather", choices=("rgba8", "image", "all"), default="rgba8",
                    help="fields gathered to rank 0 at N > 1: the rgba8 display buffer the "
                         "colour pass writes (4 B/ray, default), the f64 colour planes "
@@ -194,7 +200,15 @@ def main():
     bh, dk, cfg = c.scene()
     cam = configs.camera(args.camera)
     samples = args.weak_mode == "samples" and c.scaling != "strong"
-    plan = c.frame(1 if samples else world)
+    plan_n = world
+    if args.plan_gpus is not None:
+        if world != 1 or samples or args.plan_gpus < 1:
+            raise SystemExit("--plan-gpus N times one shard of the N-GPU plan at --gpus 1")
+        plan_n = args.plan_gpus
+        if args.shard is not None and not 0 <= args.shard < c.frame(plan_n).shards:
+            raise SystemExit(f"--shard {args.shard}: the {plan_n}-GPU plan has "
+                             f"{c.frame(plan_n).shards} shards")
+    plan = c.frame(1 if samples else plan_n)
     W, H, S, B = plan.width, plan.height, plan.shards, plan.row_block
     if samples:
         if S != 1:
@@ -311,6 +325,8 @@ def main():
             "sample_plane": (rank if args.sample is None else args.sample) if samples else None,
             "width": W,
             "height": H,
+            "plan_gpus": plan_n,
+            "shard": None if samples else shard,
             "shards": S,
             "row_block": B,
             "rays_per_frame": rays_frame,

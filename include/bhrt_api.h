@@ -331,10 +331,15 @@ int bhrt_device_count(void);
  * (1..64; 0 = per scene: 8 for RK4 at spin 0, else 64). Affects speed only. */
 void bhrt_set_refill_threshold(int lanes);
 
-/* Tuning knob: the order in which the next device camera frames of n rays claim their rays --
- * d_order, a device array holding a permutation of [0, n) (this thread; NULL or n = 0: ray id
- * order). Results are the same in any order; only the schedule changes. */
-void bhrt_set_claim_order(const int* d_order, int n);
+/* Tuning knob: the order in which this thread's next bhrt_render_frame_device calls of n rays
+ * claim their rays -- d_order, an int array on the CURRENT device holding a permutation of
+ * [0, n) (NULL or n = 0: the default order). Results are the same in any order; only the
+ * schedule changes. The array is checked to be a permutation here (one D2H copy): returns 0,
+ * or -1 (and the default order) if it is not. It applies only to device-API frames of exactly
+ * n rays on the device that was current here, never to the chunks of bhrt_render_frame[_async]
+ * host frames. libbhrt keeps the pointer: it must stay valid until the order is cleared
+ * (bhrt_set_claim_order(NULL, 0)) or replaced. */
+int bhrt_set_claim_order(const int* d_order, int n);
 
 /* update_particles (particle_sim.c:505-566) applied `steps` times in one device round trip:
  * the particle array is copied to the GPU once, stepped `steps` times by the HIP kernel and

@@ -59,7 +59,7 @@ _PROTOS = {
     "bhrt_get_stats": (C.c_int, [_P(abi.Stats), C.c_int]),
     "bhrt_device_count": (C.c_int, []),
     "bhrt_set_refill_threshold": (None, [C.c_int]),
-    "bhrt_set_claim_order": (None, [C.c_void_p, C.c_int]),
+    "bhrt_set_claim_order": (C.c_int, [C.c_void_p, C.c_int]),
     "bhrt_last_error": (C.c_char_p, []),
     "bh_initialize": (C.c_void_p, []),
     "bh_shutdown": (None, [C.c_void_p]),
@@ -166,8 +166,9 @@ def render_frame_device(bh, dk, cfg, cam, width, height, rows, method, flags, so
 
 def set_claim_order(d_order_ptr, n):
     """bhrt_set_claim_order: the claim order (device int32 permutation of [0, n)) of this
-    thread's next device camera frames of n rays; None / 0 = ray id order."""
-    load().bhrt_set_claim_order(d_order_ptr, int(n))
+    thread's next device camera frames of n rays; None / 0 = the default order. Raises if the
+    array is not a permutation of [0, n)."""
+    _check(load().bhrt_set_claim_order(d_order_ptr, int(n)), "bhrt_set_claim_order")
 
 
 def shard_rows(height, rows):

@@ -156,11 +156,41 @@ static _Thread_local devctx_t* g_ctx[BHRT_MAX_DEV];
 static _Thread_local bhrt_stats g_stats;
 static int g_refill = 0; /* 0: chosen per scene (refill_default) */
 
+/* claim order of this thread's next device camera frames (bhrt_set_claim_order): a device
+ * permutation of [0, n) on device g_order_dev, used only by bhrt_render_frame_device calls on
+ * that device for frames of exactly n rays (never by the chunks of host-buffer frames) */
 static __thread const int* g_order;
-static __thread int g_order_n;
-void bhrt_set_claim_order(const int* d_order, int n) {
-    g_order = n > 0 ? d_order : NULL;
-    g_order_n = d_order ? n : 0;
+static __thread int g_order_n, g_order_dev = -1;
+static int current_device(void);
+int bhrt_set_claim_order(const int* d_order, int n) {
+    g_order = NULL;
+    g_order_n = 0;
+    g_order_dev = -1;
+    if (!d_order || n <= 0) return 0;
+    const int dev = current_device();
+    if (dev < 0) {
+        set_err("bhrt_set_claim_order: no current HIP device");
+        return -1;
+    }
+    /* claim_ray indexes the outputs with order[position]: only a permutation is safe */
+    int* h = (int*)malloc((size_t)n * sizeof(int));
+    unsigned char* seen = (unsigned char*)calloc((size_t)n, 1);
+    int ok = h && seen &&
+             hipMemcpy(h, d_order, (size_t)n * sizeof(int), hipMemcpyDeviceToHost) == hipSuccess;
+    for (long i = 0; ok && i < n; i++) {
+        if (h[i] < 0 || h[i] >= n || seen[h[i]]) ok = 0;
+        else seen[h[i]] = 1;
+    }
+    free(h);
+    free(seen);
+    if (!ok) {
+        set_err("bhrt_set_claim_order: the order is not a device permutation of [0, %d)", n);
+        return -1;
+    }
+    g_order = d_order;
+    g_order_n = n;
+    g_order_dev = dev;
+    return 0;
 }
 
 void bhrt_set_refill_threshold(int lanes) {
@@ -639,10 +669,12 @@ static void claim_tiles(bhrt_camera_k* k, int W, int nrows) {
     }
 }
 
-int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParams* dk,
-                             const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
-                             const bhrt_rows* rows, IntegrationMethod method, int flags,
-                             const bhrt_frame_soa* out, void* stream) {
+/* use_order: whether the thread's claim order (bhrt_set_claim_order) may apply -- the public
+ * device API only; the chunks of host-buffer frames always take the default order */
+static int render_frame_device(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                               const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                               const bhrt_rows* rows, IntegrationMethod method, int flags,
+                               const bhrt_frame_soa* out, void* stream, int use_order) {
     if (check_scene(bh, cfg) || !cam || !out || W <= 0 || H <= 0) {
         if (!g_err[0]) set_err("invalid argument");
         return -1;
@@ -670,9 +702,16 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
     kp.n = nrows * W;
     kp.init = (double*)scratch;
     kp.out = *out;
-    if (g_order && g_order_n == kp.n) kp.order = g_order;
+    if (use_order && g_order && g_order_n == kp.n && g_order_dev == dev) kp.order = g_order;
     else if (method == INTEGRATOR_RK4) claim_tiles(&kp.cam, W, nrows);
     return launch(c, &kp, (hipStream_t)stream);
+}
+
+int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                             const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                             const bhrt_rows* rows, IntegrationMethod method, int flags,
+                             const bhrt_frame_soa* out, void* stream) {
+    return render_frame_device(bh, dk, cfg, cam, W, H, rows, method, flags, out, stream, 1);
 }
 
 int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
@@ -877,7 +916,6 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
 
 typedef struct {
     int active, ticket, ndev, K, shards, W, H;
-    int reaped_ticket, reaped_rc; /* a frame a later issue waited for implicitly */
     unsigned long long last_use;
     int timing;             /* BHRT_HOST_TIMING: print where the frame's time went (device 0) */
     hipEvent_t t_ev[2 + 2 * BHRT_MAX_CHUNKS];
@@ -893,6 +931,29 @@ typedef struct {
 static _Thread_local host_frame* g_frames; /* [BHRT_FRAME_SLOTS], allocated on first use */
 static _Thread_local int g_next_ticket;
 static _Thread_local unsigned long long g_frame_clock;
+/* frames a later issue completed implicitly (frame_slot), kept for their own bhrt_frame_wait:
+ * a ring of the last BHRT_REAPED results, so reaping one slot again before the caller waited
+ * on the first ticket does not lose that result */
+#define BHRT_REAPED 32
+static _Thread_local struct {
+    int ticket, rc;
+} g_reaped[BHRT_REAPED];
+static _Thread_local int g_reaped_next;
+
+/* drain every stream of the first ndev devices (keeps the current error text): a frame that
+ * failed part way may still have launches and copies queued on its slot's buffers */
+static void drain_devices(int ndev) {
+    char err[sizeof g_err];
+    memcpy(err, g_err, sizeof err);
+    for (int d = 0; d < ndev; d++) {
+        devctx_t* c = g_ctx[d];
+        if (!c || hipSetDevice(d) != hipSuccess) continue;
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->stream2);
+        (void)hipStreamSynchronize(c->copy);
+    }
+    memcpy(g_err, err, sizeof err);
+}
 
 /* Chunks per device: each chunk's copy overlaps the tracing of the next, so only the last
  * chunk's copy follows the trace; but a chunk of C2 is traced by a full-chip persistent grid,
@@ -955,6 +1016,9 @@ static int frame_complete(host_frame* f) {
         for (int k = 0; k < f->K; k++) fprintf(stderr, " chunk %d traced %.2f copied %.2f", k, tr[k], cp[k]);
         fprintf(stderr, "\n");
     }
+    /* a failed wait leaves later chunks' copies queued into the slot's staging: drain them
+     * before the slot can be reused (ensure() may reallocate what a DMA still targets) */
+    if (rc != 0) drain_devices(f->ndev);
     return rc;
 }
 
@@ -969,12 +1033,13 @@ int bhrt_frame_wait(int ticket) {
             f->active = 0;
             return frame_complete(f);
         }
-        if (f->reaped_ticket == ticket) { /* completed when a later issue needed its slot */
-            f->reaped_ticket = 0;
-            if (f->reaped_rc) set_err("frame %d failed", ticket);
-            return f->reaped_rc;
-        }
     }
+    for (int i = 0; i < BHRT_REAPED; i++)
+        if (g_reaped[i].ticket == ticket) { /* completed when a later issue needed its slot */
+            g_reaped[i].ticket = 0;
+            if (g_reaped[i].rc) set_err("frame %d failed", ticket);
+            return g_reaped[i].rc;
+        }
     set_err("frame ticket %d is not in flight", ticket);
     return -1;
 }
@@ -993,8 +1058,10 @@ static host_frame* frame_slot(void) {
     for (int s = 0; s < BHRT_FRAME_SLOTS; s++)
         if (!best || g_frames[s].ticket < best->ticket) best = &g_frames[s];
     best->active = 0;
-    best->reaped_rc = frame_complete(best);
-    best->reaped_ticket = best->ticket;
+    const int rc = frame_complete(best);
+    g_reaped[g_reaped_next].ticket = best->ticket;
+    g_reaped[g_reaped_next].rc = rc;
+    g_reaped_next = (g_reaped_next + 1) % BHRT_REAPED;
     return best;
 }
 
@@ -1002,17 +1069,8 @@ static host_frame* frame_slot(void) {
  * slot's device buffers and pinned staging, so drain every stream it used before the caller
  * sees the error (a later issue may then reallocate the slot's buffers). */
 static void frame_abort(host_frame* f, int ndev) {
-    char err[sizeof g_err];
-    memcpy(err, g_err, sizeof err);
-    for (int d = 0; d < ndev; d++) {
-        devctx_t* c = g_ctx[d];
-        if (!c || hipSetDevice(d) != hipSuccess) continue;
-        (void)hipStreamSynchronize(c->stream);
-        (void)hipStreamSynchronize(c->stream2);
-        (void)hipStreamSynchronize(c->copy);
-    }
+    drain_devices(ndev);
     f->active = 0;
-    memcpy(g_err, err, sizeof err);
 }
 
 static int frame_enqueue(host_frame* f, const BlackHoleParams* bh, const AccretionDiskParams* dk,
@@ -1058,8 +1116,8 @@ static int frame_enqueue(host_frame* f, const BlackHoleParams* bh, const Accreti
             hipStream_t st = ((k + ticket) & 1) ? c->stream2 : c->stream;
             HIP_TRY(hipSetDevice(d));
             if (f->jobs[k][d].n > 0 &&
-                bhrt_render_frame_device(bh, dk, cfg, cam, W, H, shards > 1 ? &f->rows[k][d] : NULL,
-                                         method, flags, &f->jobs[k][d].dev, st))
+                render_frame_device(bh, dk, cfg, cam, W, H, shards > 1 ? &f->rows[k][d] : NULL,
+                                    method, flags, &f->jobs[k][d].dev, st, 0))
                 return -1;
             HIP_TRY(hipEventRecord(c->fr[slot].done[k], st));
             if (f->timing && d == 0) HIP_TRY(hipEventRecord(f->t_ev[2 + 2 * k], st));

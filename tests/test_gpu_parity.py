@@ -366,6 +366,17 @@ def test_claim_order_does_not_change_results(bhrt_lib, monkeypatch, cname):
                                          bhrt_lib.soa_from_tensors(t), 0)
             torch.cuda.synchronize()
             outs.append({f: v.cpu().numpy() for f, v in t.items()})
+        # an array that is not a permutation is rejected (claim_ray would index the outputs
+        # with it) and the default order stays
+        bad = torch.zeros(n, dtype=torch.int32, device="cuda")
+        with pytest.raises(bhrt_lib.BhrtError):
+            bhrt_lib.set_claim_order(bad.data_ptr(), n)
+        # a set order applies to device-API frames only: the chunks of a host-buffer frame of
+        # the same ray count never take it
+        perm = orders[2]
+        bhrt_lib.set_claim_order(perm.data_ptr(), n)
+        host = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+        outs.append(host)
     finally:
         bhrt_lib.set_claim_order(None, 0)
     for o in outs[1:]:
@@ -487,16 +498,28 @@ def _display_u8(v):
         return (np.trunc(m * np.float32(255.0)).astype(np.int64) & 0xFF).astype(np.uint8)
 
 
-@pytest.mark.parametrize("cname", ["C2", "C4"])
-def test_display_path_rgba(bhrt_lib, oracle, cname):
+@pytest.mark.parametrize("cname,fuse", [("C2", "1"), ("C4", "1"), ("C3", "1"), ("C3", "0")])
+def test_display_path_rgba(bhrt_lib, oracle, monkeypatch, cname, fuse):
     """the visualizer's texture buffer (float RGBA with alpha 1, then
-    RGBA8 by its own conversion) produced by the colour pass, row 0 = top."""
+    RGBA8 by its own conversion) produced by the colour pass, row 0 = top. C3 (RKF45 with a
+    disk) writes the colour in the trace kernel (BHRT_FUSE_COLOUR, default on):
+    both forms are run, and must give the same buffers."""
+    monkeypatch.setenv("BHRT_FUSE_COLOUR", fuse)
     c = configs.CONFIGS[cname]
     bh, dk, cfg = c.scene()
     cam = configs.camera("B")
     W, H = 96, 54
     fields = abi.SOA_FIELDS + abi.DISPLAY_FIELDS
     got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags, fields=fields)
+    if cname == "C3":  # the other colour form gives every output bit for bit
+        monkeypatch.setenv("BHRT_FUSE_COLOUR", "0" if fuse == "1" else "1")
+        other = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags, fields=fields)
+        other_only = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags,
+                                           fields=abi.DISPLAY_FIELDS)
+        monkeypatch.setenv("BHRT_FUSE_COLOUR", fuse)
+        for f in fields:
+            assert np.array_equal(other[f], got[f], equal_nan=True), f
+        assert np.array_equal(other_only["rgba8"], got["rgba8"])
     rgb = np.stack([got["rgb_r"], got["rgb_g"], got["rgb_b"]], axis=1)
     f32 = got["rgba32f"]
     assert np.array_equal(f32[:, :3], rgb.astype(np.float32), equal_nan=True)
@@ -613,30 +636,35 @@ def test_async_frames_in_flight_equal_sync_frames(bhrt_lib):
             assert np.array_equal(arrays[f], want[f], equal_nan=True), (cname, camname, f)
 
 
-@pytest.mark.parametrize("cname", ["C1", "C2"])
+@pytest.mark.parametrize("cname", ["C1", "C2", "C3", "C4", "C5"])
 def test_full_frame_every_ray_vs_oracle(bhrt_lib, oracle, cname):
-    """Every ray of the BASELINE frame (C1 256x256, C2 1920x1080, camera B) against the
-    oracle: classes and steps exact, floats within 1e-5, NaN pattern; a mismatch is allowed
-    only on a listed knife-edge ray (oracle margin to a threshold < 1e-9).
-    C3-C5 get the same comparison from tools/full_frame_parity.py (profiles/)."""
+    """Every ray of the frame bench.py renders at N = 1 (camera B) against the oracle: C1
+    256x256, C2 and C3 1920x1080, C4 3840x2160 (8.3 M rays), C5 shard 0 of the 7680x4320
+    frame (540 rows, 4.1 M rays). Classes and steps exact, floats within 1e-5, NaN pattern; a
+    mismatch is allowed only on a listed knife-edge ray (oracle margin to a threshold < 1e-9,
+    SURVEY.md 7(f)). tools/full_frame_parity.py also runs the other seven C5 shards."""
     import torch
     c = configs.CONFIGS[cname]
     bh, dk, cfg = c.scene()
     cam = configs.camera("B")
-    W, H = c.width, c.height
-    t = {f: torch.zeros(W * H, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
+    plan = c.frame(1) if cname != "C5" else c.frame(8)
+    W, H = plan.width, plan.height
+    rows = plan.rows(0)
+    n = W * (H if rows is None else bhrt_lib.shard_rows(H, rows))
+    t = {f: torch.zeros(n, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
                         device="cuda") for f in abi.SOA_FIELDS}
-    bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+    bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags,
                                  bhrt_lib.soa_from_tensors(t), 0)
     torch.cuda.synchronize()
     got = {f: v.cpu().numpy() for f, v in t.items()}
+    del t
     want, margin = oracle.render_frame_margin(bh, dk, cfg, cam, W, H, c.method, c.flags,
-                                              threads=16)
+                                              rows=rows, threads=16)
     rep = full_frame_report(got, want, margin, sky_pinned(c.method))
     print(cname, {k: rep[k] for k in ("rays", "mismatched_rays", "knife_edge_rays",
                                       "min_margin", "max_rel_err_on_matching_rays")})
     assert rep["unexplained"] == 0, rep
-    assert rep["rays"] == W * H
+    assert rep["rays"] == n
 
 
 def test_frames_with_freed_arrays_and_pageable_copies(bhrt_lib, monkeypatch):

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-4 session A: GPU parity suite (now with every ray of C3, C4 and C5 shard 0) -> the
+# 8-GPU plans' shards timed on one GPU -> rocprofv3 kernel traces of C4 (serial frames and the
+# bench's two streams; whole image and an 8-GPU-plan shard) for the per-frame cost beside k_trace.
+set -o pipefail
+cd "$(dirname "$0")/.."
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+if [ -z "$SKIP_TESTS" ]; then
+  echo "== pytest -m gpu"
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1 \
+    || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+  tail -1 $OUT/pytest_gpu.log
+fi
+if [ -z "$SKIP_PLAN" ]; then
+  echo "== plan shards"
+  CONFIGS="${PLAN_CFGS:-C2 C4 C5}" bash tools/plan_shards.sh > $OUT/plan_shards.jsonl 2> $OUT/plan_shards.err \
+    || { echo "plan shards failed"; tail -20 $OUT/plan_shards.err; exit 1; }
+  python tools/plan_summary.py $OUT/plan_shards.jsonl --out $OUT/plan_summary.txt
+fi
+for v in ${TRACE_VARIANTS-s1 s2 p8}; do
+  case $v in
+    s1) args="--streams 1";;
+    s2) args="";;
+    p8) args="--plan-gpus 8 --shard 0";;
+  esac
+  echo "== rocprof C4 $v"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_C4_$v -o run --output-format csv -- python bench.py --config C4 --steps 20 --warmup 3 --no-cpu-baseline --no-host-path $args > $OUT/bench_prof_C4_$v.json 2> $OUT/prof_C4_$v.err \
+    || { echo "rocprof C4 $v failed"; tail -20 $OUT/prof_C4_$v.err; exit 1; }
+  python tools/frame_timeline.py $(find $OUT/prof_C4_$v -name "*kernel_trace.csv" | head -1) --skip 3 > $OUT/timeline_C4_$v.txt || true
+  cat $OUT/timeline_C4_$v.txt
+done
+echo all-done
