@@ -848,6 +848,18 @@ static int host_threads(void) {
     return t < 1 ? 1 : (t > 64 ? 64 : t);
 }
 
+/* memcpy of a large block split over OpenMP threads (one thread moves ~10-16 GB/s: a C2 batch's
+ * 100 MB of rays staged by one thread took 10 ms, longer than the whole frame's trace) */
+static void par_memcpy(void* dst, const void* src, size_t bytes, int nthreads) {
+    const size_t piece = (size_t)1 << 20;
+    const long np = (long)((bytes + piece - 1) / piece);
+#pragma omp parallel for schedule(static) num_threads(nthreads) if (np >= 4 && nthreads > 1)
+    for (long q = 0; q < np; q++) {
+        const size_t a = piece * (size_t)q;
+        memcpy((char*)dst + a, (const char*)src + a, bytes - a < piece ? bytes - a : piece);
+    }
+}
+
 static void readback_finish(const shard_job* j, const bhrt_frame_soa* host, const char* stage,
                             int W, const bhrt_rows* rows, int f_lo, int f_hi) {
     /* every wanted field of the chunk as pieces of <= 1 MB (one image row at a time when the
@@ -1296,9 +1308,11 @@ static void hit_fields(char* p, long n, bhrt_frame_soa* s) {
 #define HIT_BYTES (2 * sizeof(int32_t) + 8 * sizeof(double))
 
 /* Large batches: K contiguous chunks per device on alternating trace streams. Launching chunk
- * k first copies its rays into pinned staging (so the upload is asynchronous and overlaps the
- * chunks already tracing); each chunk's results come back on the copy stream, and the host
- * packs a chunk into hits[] as soon as it lands, with nthreads threads. */
+ * k first copies its rays into pinned staging (OpenMP threads; so the upload is asynchronous and
+ * overlaps the chunks already tracing); each chunk's results come back on the copy stream, and
+ * the host packs a chunk into hits[] as soon as it lands, with nthreads threads. The first chunk
+ * is half the size of the others, so the GPU starts tracing after half a chunk's staging.
+ * BHRT_HOST_TIMING=1 prints where a call's time went. */
 static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* bh,
                                 const AccretionDiskParams* dk, const SimulationConfig* cfg,
                                 RayTraceHit* hits, int nthreads) {
@@ -1312,11 +1326,17 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
     int K = (long)n / ndev >= (1L << 20) ? 4 : 2;
     const char* env = getenv("BHRT_HOST_CHUNKS");
     if (env && atoi(env) >= 1 && atoi(env) <= BHRT_MAX_CHUNKS) K = atoi(env);
+    const int stage_threads = host_threads();
+    const int timing = getenv("BHRT_HOST_TIMING") != NULL;
+    struct timespec tt[4];
+    clock_gettime(CLOCK_MONOTONIC, &tt[0]);
     long base[BHRT_MAX_CHUNKS + 1][BHRT_MAX_DEV]; /* chunk k of device d: [base[k][d], base[k+1][d]) */
     shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
     for (int d = 0; d < ndev; d++) {
         const long d0 = (long)n * d / ndev, d1 = (long)n * (d + 1) / ndev;
-        for (int k = 0; k <= K; k++) base[k][d] = d0 + (d1 - d0) * k / K;
+        /* chunk boundaries in units of 1/(2K - 1): the first chunk one unit, the others two */
+        for (int k = 0; k <= K; k++)
+            base[k][d] = k == 0 ? d0 : d0 + (d1 - d0) * (2 * k - 1) / (2 * K - 1);
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
         HIP_TRY(hipSetDevice(d));
@@ -1338,7 +1358,7 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
             hit_fields((char*)c->d_soa + (size_t)a * HIT_BYTES + 256 * k, m, &jobs[k][d].dev);
             if (m > 0) {
                 Ray* hr = (Ray*)c->h_rays + a;
-                memcpy(hr, rays + base[k][d], (size_t)m * sizeof(Ray));
+                par_memcpy(hr, rays + base[k][d], (size_t)m * sizeof(Ray), stage_threads);
                 HIP_TRY(hipMemcpyAsync((Ray*)c->d_rays + a, hr, (size_t)m * sizeof(Ray),
                                        hipMemcpyHostToDevice, st));
                 if (bhrt_trace_rays_device((const Ray*)c->d_rays + a, (int)m, bh, dk, cfg,
@@ -1353,23 +1373,38 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                                        hipMemcpyDeviceToHost, c->copy));
             HIP_TRY(hipEventRecord(c->chunk_copied[k], c->copy));
         }
+    clock_gettime(CLOCK_MONOTONIC, &tt[1]);
+    double wait_ms = 0.0, pack_ms = 0.0;
     for (int k = 0; k < K; k++)
         for (int d = 0; d < ndev; d++) {
             devctx_t* c = jobs[k][d].c;
             const long a = base[k][d] - base[0][d], m = jobs[k][d].n;
             HIP_TRY(hipSetDevice(d));
+            clock_gettime(CLOCK_MONOTONIC, &tt[2]);
             HIP_TRY(hipEventSynchronize(c->chunk_copied[k]));
             bhrt_frame_soa s;
             hit_fields((char*)c->h_stage + (size_t)a * HIT_BYTES, m, &s);
+            clock_gettime(CLOCK_MONOTONIC, &tt[3]);
             pack_hits(hits + base[k][d], m, &s, nthreads);
+            if (timing) {
+                struct timespec t4;
+                clock_gettime(CLOCK_MONOTONIC, &t4);
+                wait_ms += (tt[3].tv_sec - tt[2].tv_sec) * 1e3 + (tt[3].tv_nsec - tt[2].tv_nsec) * 1e-6;
+                pack_ms += (t4.tv_sec - tt[3].tv_sec) * 1e3 + (t4.tv_nsec - tt[3].tv_nsec) * 1e-6;
+            }
         }
+    if (timing)
+        fprintf(stderr, "libbhrt trace_rays_batch n=%d K=%d: stage+issue %.2f ms, wait %.2f ms, "
+                "pack %.2f ms (%d threads)\n", n, K,
+                (tt[1].tv_sec - tt[0].tv_sec) * 1e3 + (tt[1].tv_nsec - tt[0].tv_nsec) * 1e-6,
+                wait_ms, pack_ms, nthreads);
     return 0;
 }
 
 static int trace_into_hits(const Ray* rays, int n, const BlackHoleParams* bh,
                            const AccretionDiskParams* dk, const SimulationConfig* cfg,
                            RayTraceHit* hits, int nthreads) {
-    if (nthreads <= 0) nthreads = 8;
+    if (nthreads <= 0) nthreads = host_threads();
     if (n >= (1 << 16)) return trace_hits_pipelined(rays, n, bh, dk, cfg, hits, nthreads);
     char* buf = (char*)malloc(HIT_BYTES * (size_t)n);
     if (!buf) {
@@ -1406,7 +1441,7 @@ int trace_rays_batch(const Ray* rays, int n, const BlackHoleParams* bh,
         return -1;
     }
     /* num_threads: the reference's OpenMP thread count; here the host threads that pack the
-     * results into hits[] (0 = 8) */
+     * results into hits[] (0 = BHRT_HOST_THREADS, default 16) */
     if (trace_into_hits(rays, n, bh, dk, cfg, hits, num_threads) != 0) {
         for (int i = 0; i < n; i++) hits[i].result = RAY_ERROR;
         return -1;

@@ -1,5 +1,7 @@
 """trace_rays_batch (the reference's batch API: Ray[] in, RayTraceHit[] out) for the C2
-camera's 2 M rays: wall time per call with reused arrays, against the trace kernel."""
+camera's 2 M rays: wall time per call with reused arrays, against the trace kernel, for several
+chunk counts (BHRT_HOST_CHUNKS) and pack thread counts; BHRT_HOST_TIMING=1 adds libbhrt's
+per-call breakdown (staging + issue, waiting for chunks, packing) on stderr."""
 import ctypes as C
 import os
 import sys
@@ -9,35 +11,27 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
-sys.path.insert(0, os.path.join(ROOT, "oracle"))
 from bhrt import abi, configs, lib  # noqa: E402
 
 c = configs.CONFIGS["C2"]
 bh, dk, cfg = c.scene()
 cam = configs.camera("B")
 W, H = 1920, 1080
-O = __import__("oracle").oracle().lib
-O.orc_camera_ray_direction.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, C.c_int,
-                                       C.POINTER(abi.Camera), C.POINTER(abi.Vector3D)]
-rays = np.zeros(W * H, dtype=abi.RAY_DTYPE)
-rays["origin"] = (cam.position.x, cam.position.y, cam.position.z)
-d = abi.Vector3D()
-dirs = np.zeros((W * H, 3))
-for y in range(H):
-    for x in range(W):
-        O.orc_camera_ray_direction(x, y, 0.5, 0.5, W, H, C.byref(cam), C.byref(d))
-        dirs[y * W + x] = (d.x, d.y, d.z)
-rays["direction"] = dirs
+rays = configs.camera_rays(cam, W, H)
 hits = np.zeros(W * H, dtype=abi.HIT_DTYPE)
-hits[...] = 0
 L = lib.load()
-args = (rays.ctypes.data, W * H, C.byref(bh), C.byref(dk), C.byref(cfg), hits.ctypes.data, 0)
-assert L.trace_rays_batch(*args) == 0
-lib.stats(reset=True)
-t = time.perf_counter()
-for _ in range(3):
-    assert L.trace_rays_batch(*args) == 0
-dt = (time.perf_counter() - t) / 3
-st = lib.stats(reset=True)
-print(f"trace_rays_batch 2M rays: {dt * 1e3:.2f} ms/call ({W * H / dt / 1e6:.1f} Mrays/s), "
-      f"kernel {st['kernel_ms'] / 3:.2f} ms/call over {st['launches'] // 3} launches")
+for chunks in os.environ.get("CHUNKS", "4 2 3 6 8").split():
+    for threads in (0, 8):
+        os.environ["BHRT_HOST_CHUNKS"] = chunks
+        args = (rays.ctypes.data, W * H, C.byref(bh), C.byref(dk), C.byref(cfg),
+                hits.ctypes.data, threads)
+        assert L.trace_rays_batch(*args) == 0
+        lib.stats(reset=True)
+        t = time.perf_counter()
+        for _ in range(4):
+            assert L.trace_rays_batch(*args) == 0
+        dt = (time.perf_counter() - t) / 4
+        st = lib.stats(reset=True)
+        print(f"trace_rays_batch 2M rays, {chunks} chunks, num_threads {threads}: "
+              f"{dt * 1e3:.2f} ms/call ({W * H / dt / 1e6:.1f} Mrays/s), kernel "
+              f"{st['kernel_ms'] / 4:.2f} ms/call over {st['launches'] // 4} launches", flush=True)

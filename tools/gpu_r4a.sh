@@ -32,3 +32,10 @@ for v in ${TRACE_VARIANTS-s1 s2 p8}; do
   cat $OUT/timeline_C4_$v.txt
 done
 echo all-done
+if [ -z "$SKIP_BATCH" ]; then
+  echo "== batch probe"
+  BHRT_HOST_TIMING=1 timeout -k 10 300 python tools/batch_probe.py > $OUT/batch_probe.txt 2> $OUT/batch_probe.err \
+    || { echo "batch probe failed"; tail -20 $OUT/batch_probe.err; exit 1; }
+  cat $OUT/batch_probe.txt
+fi
+echo all-done-2
