@@ -486,6 +486,13 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
         s->h_lo[0] = fmax(t1, fmax(t2, t3));
         s->h_hi[0] = INFINITY;
     }
+    {
+        /* a step's nominal increment of state[2] is h * (a weighted sum of the constant
+         * state[5] whose weights' magnitudes add up to <= 1.36, RKF45's 5th order; RK4 1) */
+        const double hmax = fmax(fmax(fabs(s->h_2_5), fabs(s->h_5)), fmax(fabs(s->h_15), fabs(s->h_far)));
+        s->rot_vmax = hmax > 0.0 ? 0.78 / (hmax * 1.4) : INFINITY; /* 0.78 < pi/4 */
+        if (!(s->rot_vmax >= 0.0)) s->rot_vmax = 0.0;              /* (NaN / Inf step sizes) */
+    }
     s->max_dist = cfg->max_ray_distance;
     s->tol = cfg->tolerance;
     s->max_steps = cfg->max_integration_steps;

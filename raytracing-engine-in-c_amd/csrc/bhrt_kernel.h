@@ -44,6 +44,9 @@ typedef struct {
     int spin0;   /* blackhole->spin == 0.0 */
     int far_bounded; /* a state within 2^40 stays below 2^400 over max_steps steps, far-field
                         branch included (bhrt_api.c far_bounded; geodesic.hip repair_at_refill) */
+    double rot_vmax; /* zero-acceleration paths: a ray with |state[5]| below this turns state[2]
+                        by less than pi/4 per step for every step size (geodesic.hip
+                        rotation_trig); a ray at or above it is re-traced by the redo pass */
 } bhrt_scene_k;
 
 typedef struct {

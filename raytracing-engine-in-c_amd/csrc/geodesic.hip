@@ -175,15 +175,30 @@ __device__ __forceinline__ bool sincos_shift_wide(double a, double s0, double c0
     return true;
 }
 
-// sin(delta) and cos(delta) - 1 for |delta| <= 1/16: shift_or_eval's polynomials
+// sin(delta) and cos(delta) - 1: for |delta| <= 1/16 shift_or_eval's polynomials, above that
+// (|delta| <= pi/4) the fdlibm k_sin / k_cos ones of sincos_shift_wide
 __device__ __forceinline__ void rotation_coeffs(double delta, double& sd, double& cm1) {
-    constexpr double S1 = -0.16666666666662605, S2 = 0.00833333327878775,
-                     S3 = -0.00019839069723619096;
-    constexpr double C1 = 0.04166666666666157, C2 = -0.0013888888827212717,
-                     C3 = 2.479927034006378e-05;
     const double z = delta * delta;
-    sd = delta + (z * delta) * fmac_k(z, fmac_k(z, S3, S2), S1);
-    cm1 = z * __builtin_fma(z, fmac_k(z, fmac_k(z, C3, C2), C1), -0.5);
+    if (__builtin_expect(fabs(delta) <= 0.0625, 1)) {
+        constexpr double S1 = -0.16666666666662605, S2 = 0.00833333327878775,
+                         S3 = -0.00019839069723619096;
+        constexpr double C1 = 0.04166666666666157, C2 = -0.0013888888827212717,
+                         C3 = 2.479927034006378e-05;
+        sd = delta + (z * delta) * fmac_k(z, fmac_k(z, S3, S2), S1);
+        cm1 = z * __builtin_fma(z, fmac_k(z, fmac_k(z, C3, C2), C1), -0.5);
+        return;
+    }
+    constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                     S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                     S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                     C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                     C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double w = z * z;
+    const double r = fmac_k(z, fmac_k(z, S4, S3), S2) + z * w * fmac_k(z, S6, S5);
+    sd = delta + (z * delta) * fmac_k(z, r, S1);
+    const double rc = z * fmac_k(z, fmac_k(z, C3, C2), C1) + w * w * fmac_k(z, fmac_k(z, C6, C5), C4);
+    cm1 = z * rc - 0.5 * z;
 }
 
 // sin, cos of x given those of a nearby a, as the trace loop needs them: every RK stage after
@@ -643,8 +658,8 @@ struct Ray_ {
     double dist;
     double s1, c1, s2, c2, s3, c3;  // sin, cos of y[1], y[2], y[3] (carried)
     double zs[6];       // per-ray stage sums of components 0..2 (hoist_sums)
-    double cd_h, cd_sd, cd_cm1;  // rotation_trig: the step size the rotation is for (NaN:
-                                 // none), sin(delta) and cos(delta) - 1 of its increment
+    double cd_sd, cd_cm1;        // rotation_trig: sin(delta) and cos(delta) - 1 of the
+                                 // increment at the step size h (set with it, hcache)
     double h, h_lo, h_hi;        // hcache: the step size and the r interval it holds on
     int k;              // iterations executed
     bool far_ok;        // use_analytic_approx && impact_parameter > 0
@@ -868,9 +883,13 @@ __device__ __forceinline__ bool state_within(const Ray_& R, double bound) {
 // bit-identical (profiles/r03_ab/hcache_v33.txt). Elsewhere it measured neutral (C2, C5 --
 // where the changed code also moved some hit points by ~1e-15) or -1.4% (C3), so the chain
 // stays; k_path and the HUGE redo always select.
-template <int METHOD, bool SPIN0, bool HUGE>
+// The zero-acceleration paths (rotation_trig: C4, C5) keep it too, and form the rotation of
+// state[2]'s sin, cos for the new step size in the same rare branch: a regime change is then
+// one test per iteration instead of two.
+template <int METHOD, bool SPIN0, bool FAR, bool HUGE>
 constexpr bool hcache() {
-    return METHOD == INTEGRATOR_RK4 && !SPIN0 && !HUGE;
+    return (METHOD == INTEGRATOR_RK4 && !SPIN0 && !HUGE) ||
+           rotation_trig<METHOD, SPIN0, FAR, HUGE>();
 }
 
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
@@ -887,7 +906,7 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     // is folded into the values (host)
     const double r = R.y[1];
     double h;
-    if constexpr (hcache<METHOD, SPIN0, HUGE>()) {
+    if constexpr (hcache<METHOD, SPIN0, FAR, HUGE>()) {
         // the size is cached per ray with the r interval it holds on (Scene h_lo / h_hi): a ray
         // changes regime at most three times, so each iteration is two compares instead of the
         // three compares and three 64-bit selects of the chain (NaN r: always re-selected,
@@ -900,6 +919,23 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
             R.h = k == 0 ? hs.far_ : (k == 1 ? hs.r15 : (k == 2 ? hs.r5 : hs.r2_5));
             R.h_lo = sc.h_lo[k];
             R.h_hi = sc.h_hi[k];
+            if constexpr (rotation_trig<METHOD, SPIN0, FAR, HUGE>()) {
+                // the nominal increment of state[2] at this step size: h/6 * ((v + 2v) + 2v) + v
+                // (rk4_step) or h * sum5 (rkf45_attempt), v = state[5] (constant here). |d| <
+                // pi/4 for every ray k_trace keeps in these instantiations (|v| <
+                // Scene.rot_vmax, checked at refill; any other ray is re-traced by the HUGE
+                // pass, which advances its trig directly).
+                double d;
+                if (METHOD == INTEGRATOR_RK4) {
+                    double a = R.y[5];
+                    a = rk4_acc(a, R.y[5]);
+                    a = rk4_acc(a, R.y[5]);
+                    d = (R.h * (1.0 / 6.0)) * (a + R.y[5]);
+                } else {
+                    d = R.h * R.zs[5];
+                }
+                rotation_coeffs(d, R.cd_sd, R.cd_cm1);
+            }
         }
         h = R.h;
     } else {
@@ -927,32 +963,10 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
         // loop-carried advance alive otherwise (C5: 45 instructions of the loop)
         if (SPIN0) trig_advance(tr.a, R.y[1], R.s1, R.c1, hc);
         if constexpr (rotation_trig<METHOD, SPIN0, FAR, HUGE>()) {
-            if (__builtin_expect(!(h == R.cd_h), 0)) {  // a new regime (or none cached)
-                // the nominal increment of state[2]: h/6 * ((v + 2v) + 2v) + v (rk4_step) or
-                // h * sum5 (rkf45_attempt), v = state[5]
-                double d;
-                if (METHOD == INTEGRATOR_RK4) {
-                    double a = R.y[5];
-                    a = rk4_acc(a, R.y[5]);
-                    a = rk4_acc(a, R.y[5]);
-                    d = (h * (1.0 / 6.0)) * (a + R.y[5]);
-                } else {
-                    d = h * R.zs[5];
-                }
-                if (fabs(d) <= 0.0625) {
-                    rotation_coeffs(d, R.cd_sd, R.cd_cm1);
-                    R.cd_h = h;
-                } else {
-                    R.cd_h = __builtin_nan("");
-                }
-            }
-            if (R.cd_h == h) {
-                const double s0 = R.s2, c0 = R.c2;
-                R.s2 = __builtin_fma(c0, R.cd_sd, __builtin_fma(s0, R.cd_cm1, s0));
-                R.c2 = __builtin_fma(-s0, R.cd_sd, __builtin_fma(c0, R.cd_cm1, c0));
-            } else {
-                trig_advance(a2, R.y[2], R.s2, R.c2, hc);
-            }
+            // (the rotation for this step size was formed with it, above)
+            const double s0 = R.s2, c0 = R.c2;
+            R.s2 = __builtin_fma(c0, R.cd_sd, __builtin_fma(s0, R.cd_cm1, s0));
+            R.c2 = __builtin_fma(-s0, R.cd_sd, __builtin_fma(c0, R.cd_cm1, c0));
         } else {
             trig_advance(a2, R.y[2], R.s2, R.c2, hc);
         }
@@ -1509,13 +1523,15 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     if (repair_at_refill<METHOD, FAR, HUGE>() && kp.sc.max_steps > 0)
                         state_repair<!INL>(R, &n);
                     if (hoist_sums<METHOD, SPIN0, FAR, HUGE>()) zero_sums<METHOD>(R);
-                    if (rotation_trig<METHOD, SPIN0, FAR, HUGE>()) R.cd_h = __builtin_nan("");
-                    if (hcache<METHOD, SPIN0, HUGE>()) R.h_lo = R.h_hi = __builtin_nan("");  // select on entry
+                    if (hcache<METHOD, SPIN0, FAR, HUGE>()) R.h_lo = R.h_hi = __builtin_nan("");  // select on entry
                     // the far-field bound (repair_at_refill) not proven for this ray: it is handed
                     // to the HUGE redo pass after its first trip, like a large-argument ray (the
                     // trip's one iteration is discarded; a branch here would cost spills at
                     // every refill)
                     if (FAR && !HUGE && !(kp.sc.far_bounded && state_within(R, 0x1p40)))
+                        n.huge = true;
+                    // the rotation of state[2]'s sin, cos needs |h state[5]| < pi/4 (rotation_trig)
+                    if (rotation_trig<METHOD, SPIN0, FAR, HUGE>() && !(fabs(R.y[5]) < kp.sc.rot_vmax))
                         n.huge = true;
                     n.rays++;
                     live = true;

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-4 session A: GPU parity suite (now with every ray of C3, C4 and C5 shard 0) -> the
-# 8-GPU plans' shards timed on one GPU -> rocprofv3 kernel traces of C4 (serial frames and the
-# bench's two streams; whole image and an 8-GPU-plan shard) for the per-frame cost beside k_trace.
+# Round-4 session A: GPU parity suite (every ray of C1-C4 and C5 shard 0) -> same-box A/B of
+# kernel variants -> the 8-GPU plans' shards timed on one GPU -> rocprofv3 kernel traces of C4
+# (serial frames, the bench's two streams, an 8-GPU-plan shard) -> trace_rays_batch probe.
+# A failing test does not stop the session (rc 1); a crash, abort or time limit does.
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -9,9 +10,17 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
   echo "== pytest -m gpu"
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1 \
-    || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1
+  rc=$?
   tail -1 $OUT/pytest_gpu.log
+  grep -E "FAILED|ERROR" $OUT/pytest_gpu.log | head -20
+  [ $rc -le 1 ] || { echo "pytest rc=$rc: stopping"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+fi
+if [ -n "$AB_VARIANTS" ]; then
+  for c in ${AB_CFGS:-C4 C5}; do
+    echo "== ab $c"
+    CFG=$c VARIANTS="$AB_VARIANTS" ROUNDS=${AB_ROUNDS:-3} EXTRA="--no-host-path" bash tools/ab.sh || exit 1
+  done
 fi
 if [ -z "$SKIP_PLAN" ]; then
   echo "== plan shards"
@@ -31,11 +40,10 @@ for v in ${TRACE_VARIANTS-s1 s2 p8}; do
   python tools/frame_timeline.py $(find $OUT/prof_C4_$v -name "*kernel_trace.csv" | head -1) --skip 3 > $OUT/timeline_C4_$v.txt || true
   cat $OUT/timeline_C4_$v.txt
 done
-echo all-done
 if [ -z "$SKIP_BATCH" ]; then
   echo "== batch probe"
   BHRT_HOST_TIMING=1 timeout -k 10 300 python tools/batch_probe.py > $OUT/batch_probe.txt 2> $OUT/batch_probe.err \
     || { echo "batch probe failed"; tail -20 $OUT/batch_probe.err; exit 1; }
   cat $OUT/batch_probe.txt
 fi
-echo all-done-2
+echo all-done
