@@ -281,6 +281,23 @@ int bhrt_render_frame_device(const BlackHoleParams* blackhole, const AccretionDi
                              IntegrationMethod method, int flags,
                              const bhrt_frame_soa* device_out, void* hip_stream);
 
+/* One camera frame rendered by several GPUs and gathered on the calling thread's CURRENT device
+ * (the root) -- the north star's "image tiled across the GPUs, one gather at frame end", from C:
+ * the image is split into `shards` cyclic row-block shards of 8 rows (<= 0: one per device),
+ * shard s rendered by device (root + s) mod ndev into that device's own buffers (ndev <= 0:
+ * every visible device), and the root copies every shard straight into its image rows of
+ * device_out -- device-to-device over xGMI for the peers (peer access enabled on first use),
+ * one strided 2-D copy per field and shard. device_out: root-device buffers of width * height
+ * elements per field (NULL fields are not produced). Asynchronous on hip_stream (a root-device
+ * hipStream_t; NULL = the library's): the frame is complete when that stream's work is. A
+ * one-shard frame is bhrt_render_frame_device on the root. Replaces the reference's serial
+ * per-pixel loop (raytracer.c:795-804 / blackhole_api.c:225-250) on a multi-GPU node. */
+int bhrt_render_frame_gather(const BlackHoleParams* blackhole, const AccretionDiskParams* disk,
+                             const SimulationConfig* config, const bhrt_camera* camera,
+                             int width, int height, IntegrationMethod method, int flags,
+                             const bhrt_frame_soa* device_out, int ndev, int shards,
+                             void* hip_stream);
+
 /* Same, into HOST buffers; splits the image over every visible GPU (cyclic row blocks)
  * and returns when the frame is complete. */
 int bhrt_render_frame(const BlackHoleParams* blackhole, const AccretionDiskParams* disk,

@@ -49,6 +49,10 @@ _PROTOS = {
                                            _P(abi.SimulationConfig), _P(abi.Camera), C.c_int,
                                            C.c_int, _P(abi.Rows), C.c_int, C.c_int,
                                            _P(abi.FrameSoA), C.c_void_p]),
+    "bhrt_render_frame_gather": (C.c_int, [_P(abi.BlackHoleParams), _P(abi.AccretionDiskParams),
+                                           _P(abi.SimulationConfig), _P(abi.Camera), C.c_int,
+                                           C.c_int, C.c_int, C.c_int, _P(abi.FrameSoA), C.c_int,
+                                           C.c_int, C.c_void_p]),
     "bhrt_trace_rays": (C.c_int, [C.c_void_p, C.c_int, _P(abi.BlackHoleParams),
                                   _P(abi.AccretionDiskParams), _P(abi.SimulationConfig), C.c_int,
                                   C.c_int, _P(abi.FrameSoA)]),
@@ -162,6 +166,17 @@ def render_frame_device(bh, dk, cfg, cam, width, height, rows, method, flags, so
                                            height, _ptr(rows), method, flags, C.byref(soa),
                                            C.c_void_p(stream) if stream else None),
            "bhrt_render_frame_device")
+
+
+def render_frame_gather(bh, dk, cfg, cam, width, height, method, flags, soa, ndev=0, shards=0,
+                        stream=None):
+    """bhrt_render_frame_gather: the frame rendered by ndev devices in `shards` cyclic shards and
+    gathered into root-device SoA buffers (the current device) on a hipStream_t."""
+    _check(load().bhrt_render_frame_gather(_ptr(bh), _ptr(dk), _ptr(cfg), _ptr(cam), width,
+                                           height, method, flags, C.byref(soa), int(ndev),
+                                           int(shards),
+                                           C.c_void_p(stream) if stream else None),
+           "bhrt_render_frame_gather")
 
 
 def set_claim_order(d_order_ptr, n):

@@ -150,6 +150,13 @@ typedef struct {
     hipEvent_t span_ref;
     int span_on;
     double span_lo, span_hi;
+    /* bhrt_render_frame_gather: this device's shard buffers; g_done = its shards rendered;
+     * g_wait = the root event after which the last gather's copies have read d_gather */
+    void* d_gather;
+    size_t cap_gather;
+    hipEvent_t g_done, g_copied, g_wait;
+    int g_wait_pending;
+    unsigned long long peer_on; /* bit d: peer access to device d enabled from this device */
 } devctx_t;
 
 static _Thread_local devctx_t* g_ctx[BHRT_MAX_DEV];
@@ -920,6 +927,155 @@ static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_
     if (readback_issue(j, host, (char*)c->h_stage, c->stream, NULL, NULL, NULL)) return -1;
     HIP_TRY(hipStreamSynchronize(c->stream));
     readback_finish(j, host, (const char*)c->h_stage, W, rows, 0, BHRT_NFIELDS);
+    return 0;
+}
+
+/* ---- multi-device device frames (bhrt_render_frame_gather) ---- */
+#define BHRT_GATHER_MAX_SHARDS 64
+
+static int lazy_event(hipEvent_t* e) {
+    if (*e) return 0;
+    HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return 0;
+}
+
+/* shard s's rows of field f (element size fs) from its shard buffer src into their image rows
+ * of dst: the shard's full 8-row blocks are one strided 2-D copy (block j -> image block
+ * j * S + s), the frame's last, partial block one more copy. Peer memory goes over xGMI. */
+static int gather_field(char* dst, const char* src, size_t fs, int W, int H, int B, int s, int S,
+                        int src_dev, devctx_t* root, hipStream_t rs) {
+    const size_t wb = fs * (size_t)W, blk = wb * (size_t)B;
+    const int nbf = H / B; /* full blocks of the image */
+    const int nfull = nbf > s ? (nbf - 1 - s) / S + 1 : 0;
+    const int peer = src_dev != root->device;
+    if (peer && !(root->peer_on >> src_dev & 1ull)) {
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, root->device, src_dev) == hipSuccess && can) {
+            hipError_t e = hipDeviceEnablePeerAccess(src_dev, 0);
+            if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) root->peer_on |= 1ull << src_dev;
+            (void)hipGetLastError();
+        }
+    }
+    if (!peer || (root->peer_on >> src_dev & 1ull)) {
+        if (nfull > 0)
+            HIP_TRY(hipMemcpy2DAsync(dst + (size_t)s * blk, (size_t)S * blk, src, blk, blk,
+                                     (size_t)nfull, hipMemcpyDeviceToDevice, rs));
+    } else { /* no peer mapping: one runtime peer copy per block */
+        for (int j = 0; j < nfull; j++)
+            HIP_TRY(hipMemcpyPeerAsync(dst + ((size_t)j * S + s) * blk, root->device,
+                                       src + (size_t)j * blk, src_dev, blk, rs));
+    }
+    if (H % B && nbf % S == s) { /* the partial last block is this shard's */
+        const size_t rows = (size_t)(H - nbf * B), off = (size_t)(nbf / S) * blk;
+        if (!peer || (root->peer_on >> src_dev & 1ull))
+            HIP_TRY(hipMemcpyAsync(dst + (size_t)nbf * blk, src + off, rows * wb,
+                                   hipMemcpyDeviceToDevice, rs));
+        else
+            HIP_TRY(hipMemcpyPeerAsync(dst + (size_t)nbf * blk, root->device, src + off, src_dev,
+                                       rows * wb, rs));
+    }
+    return 0;
+}
+
+int bhrt_render_frame_gather(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                             const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                             IntegrationMethod method, int flags, const bhrt_frame_soa* out,
+                             int ndev_req, int shards_req, void* stream) {
+    if (check_scene(bh, cfg) || !cam || !out || W <= 0 || H <= 0) {
+        if (!g_err[0]) set_err("invalid argument");
+        return -1;
+    }
+    if ((long)W * H > 0x7fffffffL) {
+        set_err("frame too large (%d x %d)", W, H);
+        return -1;
+    }
+    if ((out->rgb_r || out->rgb_g || out->rgb_b) && !(out->rgb_r && out->rgb_g && out->rgb_b)) {
+        set_err("rgb output needs all of rgb_r/g/b");
+        return -1;
+    }
+    const int total = bhrt_device_count();
+    if (total <= 0) {
+        set_err("no HIP device available (libbhrt has no CPU path)");
+        return -1;
+    }
+    const int root = current_device();
+    if (root < 0 || root >= total) {
+        set_err("the current device %d is not one libbhrt drives", root);
+        return -1;
+    }
+    const int B = 8;
+    int ndev = ndev_req > 0 && ndev_req < total ? ndev_req : total;
+    int S = shards_req > 0 ? shards_req : ndev;
+    if (S > BHRT_GATHER_MAX_SHARDS) S = BHRT_GATHER_MAX_SHARDS;
+    while (S > 1 && H < S * B) S--; /* every shard at least one row block */
+    if (ndev > S) ndev = S;
+    devctx_t* rc = ctx_get(root);
+    if (!rc) return -1;
+    hipStream_t rs = stream ? (hipStream_t)stream : rc->stream;
+    if (S == 1)
+        return render_frame_device(bh, dk, cfg, cam, W, H, NULL, method, flags, out, rs, 0);
+    const bhrt_frame_soa fields = device_fields(out, (int)method, dk != NULL);
+    bhrt_frame_soa shard_soa[BHRT_GATHER_MAX_SHARDS];
+    int rc_all = 0;
+    for (int k = 0; k < ndev && rc_all == 0; k++) { /* every device renders its shards */
+        const int d = (root + k) % total;
+        devctx_t* c = ctx_get(d);
+        if (!c || hipSetDevice(d) != hipSuccess) {
+            if (c) set_err("hipSetDevice(%d) failed", d);
+            rc_all = -1;
+            break;
+        }
+        hipStream_t st = k == 0 ? rs : c->stream;
+        size_t bytes = 0;
+        for (int s = k; s < S; s += ndev) {
+            const bhrt_rows r = {B, s, S};
+            bytes += soa_bytes(&fields, (long)bhrt_shard_rows(H, &r) * W);
+        }
+        /* the last gather's copies must have read this device's shard buffers */
+        if (c->g_wait_pending && hipStreamWaitEvent(st, c->g_wait, 0) != hipSuccess) {
+            set_err("hipStreamWaitEvent failed");
+            rc_all = -1;
+            break;
+        }
+        if (ensure(&c->d_gather, &c->cap_gather, bytes ? bytes : 256, 0) || lazy_event(&c->g_done) ||
+            lazy_event(&c->g_copied)) {
+            rc_all = -1;
+            break;
+        }
+        char* p = (char*)c->d_gather;
+        for (int s = k; s < S && rc_all == 0; s += ndev) {
+            const bhrt_rows r = {B, s, S};
+            soa_carve(&p, &fields, (long)bhrt_shard_rows(H, &r) * W, &shard_soa[s]);
+            rc_all = render_frame_device(bh, dk, cfg, cam, W, H, &r, method, flags, &shard_soa[s],
+                                         st, 0);
+        }
+        if (rc_all == 0 && k > 0 && hipEventRecord(c->g_done, st) != hipSuccess) {
+            set_err("hipEventRecord failed");
+            rc_all = -1;
+        }
+    }
+    if (hipSetDevice(root) != hipSuccess) {
+        set_err("hipSetDevice(%d) failed", root);
+        return -1;
+    }
+    if (rc_all) return -1;
+    for (int k = 1; k < ndev; k++) /* the root's copies follow every peer's render */
+        HIP_TRY(hipStreamWaitEvent(rs, g_ctx[(root + k) % total]->g_done, 0));
+    for (int s = 0; s < S; s++) {
+        const int d = (root + s % ndev) % total;
+        for (int f = 0; f < BHRT_NFIELDS; f++) {
+            char* dst = (char*)*soa_slot((bhrt_frame_soa*)out, f);
+            const char* src = (const char*)*soa_slot(&shard_soa[s], f);
+            if (dst && src && gather_field(dst, src, k_fsize[f], W, H, B, s, S, d, rc, rs))
+                return -1;
+        }
+    }
+    HIP_TRY(hipEventRecord(rc->g_copied, rs));
+    for (int k = 0; k < ndev; k++) {
+        devctx_t* c = g_ctx[(root + k) % total];
+        c->g_wait = rc->g_copied;
+        c->g_wait_pending = 1;
+    }
     return 0;
 }
 

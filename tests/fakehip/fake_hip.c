@@ -22,6 +22,7 @@ struct ihipStream_t {
 struct ihipEvent_t {
     int dev;
     double t;
+    int recorded;
 };
 
 static int n_devices(void) {
@@ -209,7 +210,9 @@ hipError_t hipStreamSynchronize(hipStream_t s) {
 hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned flags) {
     (void)flags;
     check_stream(s);
-    if (e->dev != g_dev) FAIL("cross-device event wait");
+    /* a wait on another device's event is valid HIP (bhrt_render_frame_gather: the root's
+     * copies wait for every peer's render); it must have been recorded */
+    if (e->dev != g_dev && !e->recorded) FAIL("cross-device wait on an event never recorded");
     return hipSuccess;
 }
 hipError_t hipEventCreate(hipEvent_t* e) {
@@ -224,6 +227,22 @@ hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned flags) {
 hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
     check_stream(s);
     if (e->dev != g_dev) FAIL("event of device %d recorded on device %d", e->dev, g_dev);
+    e->recorded = 1;
+    return hipSuccess;
+}
+
+/* peer access: device-to-device copies may read a peer's memory once it is enabled from the
+ * current device */
+static _Thread_local unsigned char g_peer[64][64];
+hipError_t hipDeviceCanAccessPeer(int* can, int dev, int peer) {
+    *can = dev != peer && dev < n_devices() && peer < n_devices();
+    return hipSuccess;
+}
+hipError_t hipDeviceEnablePeerAccess(int peer, unsigned flags) {
+    (void)flags;
+    if (peer == g_dev || peer >= n_devices()) return ret(hipErrorInvalidDevice);
+    if (g_peer[g_dev][peer]) return ret(hipErrorPeerAccessAlreadyEnabled);
+    g_peer[g_dev][peer] = 1;
     return hipSuccess;
 }
 hipError_t hipEventSynchronize(hipEvent_t e) {
@@ -241,7 +260,10 @@ hipError_t hipEventElapsedTime(float* ms, hipEvent_t a, hipEvent_t b) {
 static void check_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind, int async) {
     if (kind == hipMemcpyDeviceToHost || kind == hipMemcpyDeviceToDevice) {
         const int k = kind_of(src, n);
-        if (k != g_dev) FAIL("copy source %p (%zu B) is not device-%d memory (kind %d)", src, n, g_dev, k);
+        const int peer_ok = kind == hipMemcpyDeviceToDevice && k >= 0 && g_peer[g_dev][k];
+        if (k != g_dev && !peer_ok)
+            FAIL("copy source %p (%zu B) is not device-%d memory nor an enabled peer's (kind %d)",
+                 src, n, g_dev, k);
     }
     if (kind == hipMemcpyHostToDevice || kind == hipMemcpyDeviceToDevice) {
         const int k = kind_of(dst, n);
@@ -272,6 +294,14 @@ hipError_t hipMemcpy2DAsync(void* dst, size_t dpitch, const void* src, size_t sp
                    kind == hipMemcpyDeviceToHost);
         memcpy((char*)dst + r * dpitch, (const char*)src + r * spitch, width);
     }
+    return hipSuccess;
+}
+hipError_t hipMemcpyPeerAsync(void* dst, int dst_dev, const void* src, int src_dev, size_t n,
+                              hipStream_t s) {
+    check_stream(s);
+    if (kind_of(dst, n) != dst_dev || kind_of(src, n) != src_dev)
+        FAIL("peer copy %p (device %d) <- %p (device %d): wrong devices", dst, dst_dev, src, src_dev);
+    memcpy(dst, src, n);
     return hipSuccess;
 }
 hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t s) {

@@ -14,6 +14,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <hip/hip_runtime_api.h>
+
 #include "bhrt_api.h"
 #include "bhrt_kernel.h"
 
@@ -197,6 +199,44 @@ static void run(BlackHoleParams* bh, SimulationConfig* cfg, AccretionDiskParams*
             check_frame(&h[k], n, "async frame");
             soa_free(&h[k]);
         }
+    }
+    /* device frames gathered on a root device (bhrt_render_frame_gather): every root, one
+     * shard per device and more shards than devices, uneven heights (a partial last block) */
+    {
+        const int gsz[][2] = {{64, 40}, {333, 77}, {200, 123}};
+        const int gshards[] = {0, 3, 5};
+        for (int root = 0; root < 2; root++)
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) {
+                    const int W = gsz[i][0], H = gsz[i][1];
+                    const long n = (long)W * H;
+                    const unsigned mask = j == 1 ? RGB_DISPLAY : ALL;
+                    CHECK(hipSetDevice(root) == hipSuccess, "set root");
+                    bhrt_frame_soa dev;
+                    memset(&dev, 0, sizeof dev);
+                    void** slot = (void**)&dev;
+                    for (int f = 0; f < 15; f++)
+                        if (mask >> f & 1) CHECK(hipMalloc(&slot[f], fsize[f] * n) == hipSuccess, "malloc");
+                    char what[96];
+                    snprintf(what, sizeof what, "thread %d gather root %d %dx%d shards %d", tid, root,
+                             W, H, gshards[j]);
+                    CHECK(bhrt_render_frame_gather(bh, dk, cfg, &cam, W, H, INTEGRATOR_RK4, 0, &dev,
+                                                   0, gshards[j], NULL) == 0,
+                          "%s: %s", what, bhrt_last_error());
+                    int cur = -1;
+                    CHECK(hipGetDevice(&cur) == hipSuccess && cur == root, "%s: root stays current", what);
+                    host_soa h = soa_new(n, mask, 0);
+                    void** hs = (void**)&h.soa;
+                    for (int f = 0; f < 15; f++)
+                        if (slot[f]) {
+                            CHECK(hipMemcpy(hs[f], slot[f], fsize[f] * n, hipMemcpyDeviceToHost) ==
+                                      hipSuccess, "readback");
+                            hipFree(slot[f]);
+                        }
+                    check_frame(&h, n, what);
+                    soa_free(&h);
+                }
+        CHECK(hipSetDevice(0) == hipSuccess, "reset device");
     }
     /* ray batches: SoA split over the devices, and the pipelined RayTraceHit path */
     for (int pass = 0; pass < 2; pass++) {

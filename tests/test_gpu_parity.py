@@ -384,6 +384,47 @@ def test_claim_order_does_not_change_results(bhrt_lib, monkeypatch, cname):
             assert np.array_equal(o[f], outs[0][f], equal_nan=True), f
 
 
+@pytest.mark.parametrize("cname", ["C2", "C4"])
+def test_gather_frame_equals_device_frame(bhrt_lib, cname):
+    """bhrt_render_frame_gather: the frame in 1, 2, 3 and 5 cyclic shards,
+    each rendered into its device's shard buffer and copied straight into its image rows on the
+    root (one 2-D copy per field and shard, plus the partial last block: 412 rows = 51.5
+    blocks), equals the one-launch device frame bit for bit, every field and the display
+    buffers. On a one-GPU box every shard is the root's (same-device copies); the peer path
+    (xGMI copies, cross-device ordering) runs on the simulated devices of
+    tests/test_multidevice_host.py."""
+    import torch
+    c = configs.CONFIGS[cname]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera("B")
+    W, H = 320, 412
+    fields = abi.SOA_FIELDS + abi.DISPLAY_FIELDS
+
+    def new():
+        t = {}
+        for f in fields:
+            dt = {"result": torch.int32, "steps": torch.int32, "rgba32f": torch.float32,
+                  "rgba8": torch.uint8}.get(f, torch.float64)
+            shape = (W * H, 4) if f in abi.DISPLAY_FIELDS else (W * H,)
+            t[f] = torch.full(shape, 7, dtype=dt, device="cuda")
+        return t
+    ref = new()
+    bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                 bhrt_lib.soa_from_tensors(ref), 0)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    for shards in (1, 2, 3, 5):
+        t = new()
+        torch.cuda.synchronize()
+        bhrt_lib.render_frame_gather(bh, dk, cfg, cam, W, H, c.method, c.flags,
+                                     bhrt_lib.soa_from_tensors(t), 0, shards, s.cuda_stream)
+        s.synchronize()
+        for f in fields:
+            assert torch.equal(t[f], ref[f]) or (
+                t[f].is_floating_point() and
+                bool(((t[f] == ref[f]) | (t[f].isnan() & ref[f].isnan())).all())), (shards, f)
+
+
 def test_empty_and_degenerate_inputs(bhrt_lib):
     bh, cfg = abi.black_hole(), abi.sim_config()
     r = bhrt_lib.trace_rays(np.zeros(0, dtype=abi.RAY_DTYPE), bh, None, cfg)
