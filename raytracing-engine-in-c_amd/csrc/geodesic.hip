@@ -1226,6 +1226,9 @@ __device__ __forceinline__ void store_colour(const bhrt_frame_soa& s, int i, dou
 #ifndef BHRT_COLD_KP
 #define BHRT_COLD_KP 1
 #endif
+#ifndef BHRT_UNIFORM_TRIP
+#define BHRT_UNIFORM_TRIP 0
+#endif
 typedef const __attribute__((address_space(4))) bhrt_kparams kparams_as4;
 // (k_trace's only argument: it starts the kernel argument segment)
 __device__ __forceinline__ const bhrt_kparams& cold(const bhrt_kparams&) {
@@ -1553,10 +1556,22 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             // further iterations in the same trip for rays that go on: the loop's hand-over
             // copies between iterations (state, point, distance, carried sin/cos) fold away. A
             // lane's iterations are the same either way; only its refill point moves.
+#if BHRT_UNIFORM_TRIP
+            // wave-uniform guard: the trip goes on only while EVERY live lane does, so the next
+            // iteration runs on the same exec mask -- no per-lane region around it, and no
+            // copies of the values a lane that stopped must keep (they are copied once, on the
+            // trip's exit edge, instead of after every iteration)
+#pragma unroll
+            for (int u = 1; u < unroll_n<METHOD, SPIN0, HUGE>(); u++) {
+                if (__ballot(term != T_NONE || n.huge) != 0ull) break;
+                term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, hsel);
+            }
+#else
 #pragma unroll
             for (int u = 1; u < unroll_n<METHOD, SPIN0, HUGE>(); u++)
                 if (term == T_NONE && !n.huge)
                     term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, hsel);
+#endif
             if (METHOD == INTEGRATOR_RK4 && (term != T_NONE || (!HUGE && n.huge)))
                 n.iters += R.k;  // every RK4 iteration moves, so R.k = iterations executed
             if (!HUGE && n.huge) {  // hand the ray to the HUGE instantiation

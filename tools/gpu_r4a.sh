@@ -16,6 +16,12 @@ if [ -z "$SKIP_TESTS" ]; then
   grep -E "FAILED|ERROR" $OUT/pytest_gpu.log | head -20
   [ $rc -le 1 ] || { echo "pytest rc=$rc: stopping"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 fi
+for v in $BITEXACT_VARIANTS; do  # every field of full frames: in-tree library vs ab/libbhrt_$v.so
+  echo "== bitexact in-tree vs $v"
+  REF=$v CONFIGS="${BITEXACT_CFGS:-C2 C3 C4 C5}" bash tools/ab_bitexact.sh > $OUT/bitexact_$v.txt 2>&1 \
+    || { echo "bitexact $v failed"; tail -20 $OUT/bitexact_$v.txt; exit 1; }
+  cat $OUT/bitexact_$v.txt
+done
 if [ -n "$AB_VARIANTS" ]; then
   for c in ${AB_CFGS:-C4 C5}; do
     echo "== ab $c"
