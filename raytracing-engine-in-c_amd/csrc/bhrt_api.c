@@ -93,6 +93,10 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 #define BHRT_RING 64        /* control blocks per context             */
 #define BHRT_CTL_WORDS 8    /* u64 per control block (64 B)           */
 #define BHRT_QWORDS ((1 << BHRT_MAX_QUEUE_BITS) * BHRT_QUEUE_STRIDE_MAX) /* queue heads per block */
+/* a launch's control block and its ray-queue heads are one region (zeroed by ONE memset per
+ * launch): 64 B of counters, padding to 256 B, then the queue heads */
+#define BHRT_QHEAD_OFF 32 /* u64 words */
+#define BHRT_SLOT_WORDS (BHRT_QHEAD_OFF + BHRT_QWORDS)
 #define BHRT_MAX_CHUNKS 8   /* host-buffer frames: pipelined chunks per device            */
 #define BHRT_SCRATCH_SLOTS 4
 #define BHRT_FRAME_SLOTS 3  /* host-buffer frames in flight per thread (bhrt_render_frame_async) */
@@ -107,8 +111,7 @@ typedef struct {
 typedef struct {
     int device;
     hipStream_t stream;
-    unsigned long long* d_ctl; /* BHRT_RING x BHRT_CTL_WORDS */
-    unsigned long long* d_q;   /* BHRT_RING x BHRT_QWORDS: ray-queue heads per control block */
+    unsigned long long* d_ctl; /* BHRT_RING x BHRT_SLOT_WORDS: control block + queue heads */
     pending_t pend[BHRT_RING];
     int npend, next_slot;
     hipEvent_t evpool[2 * BHRT_RING];
@@ -276,10 +279,8 @@ static devctx_t* ctx_get(int device) {
     if (!c) return NULL;
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void**)&c->d_ctl, BHRT_RING * BHRT_CTL_WORDS * sizeof(unsigned long long)) !=
-            hipSuccess ||
-        hipMalloc((void**)&c->d_q, (size_t)BHRT_RING * BHRT_QWORDS * sizeof(unsigned long long)) !=
-            hipSuccess) {
+        hipMalloc((void**)&c->d_ctl,
+                  (size_t)BHRT_RING * BHRT_SLOT_WORDS * sizeof(unsigned long long)) != hipSuccess) {
         set_err("cannot create HIP stream / control blocks on device %d", device);
         free(c);
         return NULL;
@@ -373,7 +374,10 @@ static int harvest(devctx_t* c) {
     unsigned long long h[BHRT_RING * BHRT_CTL_WORDS];
     HIP_TRY(hipSetDevice(c->device));
     for (int i = 0; i < c->npend; i++) HIP_TRY(hipEventSynchronize(c->pend[i].ev1));
-    HIP_TRY(hipMemcpy(h, c->d_ctl, sizeof h, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy2D(h, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+                        BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                        BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
+                        hipMemcpyDeviceToHost));
     for (int i = 0; i < c->npend; i++) {
         float ms = 0.f, t0 = 0.f, t1 = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, c->pend[i].ev0, c->pend[i].ev1));
@@ -595,11 +599,11 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     if (c->npend == BHRT_RING && harvest(c) != 0) return -1;
     int slot = c->next_slot;
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
-    kp->ctl = c->d_ctl + (size_t)slot * BHRT_CTL_WORDS;
-    kp->qhead = c->d_q + (size_t)slot * BHRT_QWORDS;
-    HIP_TRY(hipMemsetAsync(kp->ctl, 0, BHRT_CTL_WORDS * sizeof(unsigned long long), stream));
-    HIP_TRY(hipMemsetAsync(kp->qhead, 0,
-                           ((size_t)kp->queue_stride << kp->queue_bits) * sizeof(unsigned long long),
+    kp->ctl = c->d_ctl + (size_t)slot * BHRT_SLOT_WORDS;
+    kp->qhead = kp->ctl + BHRT_QHEAD_OFF;
+    HIP_TRY(hipMemsetAsync(kp->ctl, 0,
+                           (BHRT_QHEAD_OFF + ((size_t)kp->queue_stride << kp->queue_bits)) *
+                               sizeof(unsigned long long),
                            stream));
     if (!c->span_on) {
         HIP_TRY(hipEventRecord(c->span_ref, stream));

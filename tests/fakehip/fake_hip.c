@@ -304,6 +304,15 @@ hipError_t hipMemcpyPeerAsync(void* dst, int dst_dev, const void* src, int src_d
     memcpy(dst, src, n);
     return hipSuccess;
 }
+hipError_t hipMemcpy2D(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                       size_t height, hipMemcpyKind kind) {
+    if (width > dpitch || width > spitch) FAIL("2-D copy wider than its pitch");
+    for (size_t r = 0; r < height; r++) {
+        check_copy((char*)dst + r * dpitch, (const char*)src + r * spitch, width, kind, 0);
+        memcpy((char*)dst + r * dpitch, (const char*)src + r * spitch, width);
+    }
+    return hipSuccess;
+}
 hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t s) {
     check_stream(s);
     if (kind_of(p, n) != g_dev) FAIL("memset of %p: not device-%d memory", p, g_dev);
