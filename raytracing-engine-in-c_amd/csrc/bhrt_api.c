@@ -237,8 +237,8 @@ static int env_int(const char* name, int dflt) {
 /* Where the trace kernel writes the colour outputs at each ray's exit, from the state in
  * registers (bhrt_colour_in_trace), the separate pass's inputs -- result and hit point -- need
  * not exist on the device. BHRT_FUSE_COLOUR=0 keeps the separate colour pass (A/B). */
-static int colour_fused(int method, int has_disk) {
-    return BHRT_COLOUR_IN_TRACE(method, has_disk) && env_int("BHRT_FUSE_COLOUR", 1) != 0;
+static int colour_fused(int method, int has_disk, int spin) {
+    return BHRT_COLOUR_IN_TRACE(method, has_disk, spin) && env_int("BHRT_FUSE_COLOUR", 1) != 0;
 }
 
 static void claim_policy(bhrt_kparams* kp) {
@@ -521,7 +521,8 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
     }
     kp->refill = g_refill ? g_refill : refill_default(s);
     claim_policy(kp);
-    kp->colour_fused = colour_fused((int)method, dk != NULL);
+    kp->colour_fused = colour_fused((int)method, dk != NULL, bh->spin != 0.0);
+    kp->skip_redo = env_int("BHRT_SKIP_REDO", 1) != 0;
     kp->cam.rows.row_block = 1;
     kp->cam.rows.num_shards = 1;
     return 0;
@@ -651,12 +652,12 @@ static int check_scene(const BlackHoleParams* bh, const SimulationConfig* cfg) {
 }
 
 /* the colour pass (rgb and/or the display fields) reads result and the hit point */
-static int colour_args_bad(const bhrt_frame_soa* out, int method, int has_disk) {
+static int colour_args_bad(const bhrt_frame_soa* out, int method, int has_disk, int spin) {
     if ((out->rgb_r || out->rgb_g || out->rgb_b) && !(out->rgb_r && out->rgb_g && out->rgb_b)) {
         set_err("rgb output needs all of rgb_r/g/b");
         return 1;
     }
-    if ((out->rgb_r || out->rgba32f || out->rgba8) && !colour_fused(method, has_disk) &&
+    if ((out->rgb_r || out->rgba32f || out->rgba8) && !colour_fused(method, has_disk, spin) &&
         (!out->result || !out->hit_x || !out->hit_y)) {
         set_err("colour outputs need result and hit_x/hit_y (separate colour pass)");
         return 1;
@@ -705,7 +706,7 @@ static int render_frame_device(const BlackHoleParams* bh, const AccretionDiskPar
     int dev = current_device();
     devctx_t* c = ctx_get(dev);
     if (!c) return -1;
-    if (colour_args_bad(out, (int)method, dk != NULL)) return -1;
+    if (colour_args_bad(out, (int)method, dk != NULL, bh->spin != 0.0)) return -1;
     void* scratch = stream_scratch(c, stream ? (hipStream_t)stream : c->stream,
                                    (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) *
                                        (size_t)nrows * (size_t)W);
@@ -740,7 +741,7 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
         if (!g_err[0]) set_err("invalid argument");
         return -1;
     }
-    if (colour_args_bad(out, (int)method, dk != NULL)) return -1;
+    if (colour_args_bad(out, (int)method, dk != NULL, bh->spin != 0.0)) return -1;
     devctx_t* c = ctx_get(current_device());
     if (!c) return -1;
     void* scratch = stream_scratch(c, stream ? (hipStream_t)stream : c->stream,
@@ -762,11 +763,13 @@ static const size_t k_fsize[BHRT_NFIELDS] = {4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8,
 static void** soa_slot(bhrt_frame_soa* s, int f) { return ((void**)s) + f; }
 
 /* the fields a device SoA needs for the fields `want_in` requests */
-static bhrt_frame_soa device_fields(const bhrt_frame_soa* want_in, int method, int has_disk) {
+static bhrt_frame_soa device_fields(const bhrt_frame_soa* want_in, int method, int has_disk,
+                                    int spin) {
     bhrt_frame_soa want_buf = *want_in;
     if (want_buf.rgb_r || want_buf.rgb_g || want_buf.rgb_b) /* written together */
         want_buf.rgb_r = want_buf.rgb_g = want_buf.rgb_b = (double*)1;
-    if ((want_buf.rgb_r || want_buf.rgba32f || want_buf.rgba8) && !colour_fused(method, has_disk)) {
+    if ((want_buf.rgb_r || want_buf.rgba32f || want_buf.rgba8) &&
+        !colour_fused(method, has_disk, spin)) {
         /* the separate colour pass reads these */
         if (!want_buf.result) want_buf.result = (int32_t*)1;
         if (!want_buf.hit_x) want_buf.hit_x = (double*)1;
@@ -794,8 +797,8 @@ static void soa_carve(char** p, const bhrt_frame_soa* fields, long n, bhrt_frame
 
 /* carve a device SoA for n rays out of c->d_soa, for the fields `want` requests */
 static int device_soa(devctx_t* c, long n, const bhrt_frame_soa* want_in, int method,
-                      int has_disk, bhrt_frame_soa* dev) {
-    const bhrt_frame_soa fields = device_fields(want_in, method, has_disk);
+                      int has_disk, int spin, bhrt_frame_soa* dev) {
+    const bhrt_frame_soa fields = device_fields(want_in, method, has_disk, spin);
     const size_t bytes = soa_bytes(&fields, n);
     if (ensure(&c->d_soa, &c->cap_soa, bytes ? bytes : 256, 0)) return -1;
     char* p = (char*)c->d_soa;
@@ -864,18 +867,6 @@ static int host_threads(void) {
 #endif
     }
     return t < 1 ? 1 : (t > 64 ? 64 : t);
-}
-
-/* memcpy of a large block split over OpenMP threads (one thread moves ~10-16 GB/s: a C2 batch's
- * 100 MB of rays staged by one thread took 10 ms, longer than the whole frame's trace) */
-static void par_memcpy(void* dst, const void* src, size_t bytes, int nthreads) {
-    const size_t piece = (size_t)1 << 20;
-    const long np = (long)((bytes + piece - 1) / piece);
-#pragma omp parallel for schedule(static) num_threads(nthreads) if (np >= 4 && nthreads > 1)
-    for (long q = 0; q < np; q++) {
-        const size_t a = piece * (size_t)q;
-        memcpy((char*)dst + a, (const char*)src + a, bytes - a < piece ? bytes - a : piece);
-    }
 }
 
 static void readback_finish(const shard_job* j, const bhrt_frame_soa* host, const char* stage,
@@ -1018,7 +1009,7 @@ int bhrt_render_frame_gather(const BlackHoleParams* bh, const AccretionDiskParam
     hipStream_t rs = stream ? (hipStream_t)stream : rc->stream;
     if (S == 1)
         return render_frame_device(bh, dk, cfg, cam, W, H, NULL, method, flags, out, rs, 0);
-    const bhrt_frame_soa fields = device_fields(out, (int)method, dk != NULL);
+    const bhrt_frame_soa fields = device_fields(out, (int)method, dk != NULL, bh->spin != 0.0);
     bhrt_frame_soa shard_soa[BHRT_GATHER_MAX_SHARDS];
     int rc_all = 0;
     for (int k = 0; k < ndev && rc_all == 0; k++) { /* every device renders its shards */
@@ -1264,7 +1255,7 @@ static int frame_enqueue(host_frame* f, const BlackHoleParams* bh, const Accreti
         HIP_TRY(hipSetDevice(0));
         for (int i = 0; i < 2 + 2 * BHRT_MAX_CHUNKS; i++) HIP_TRY(hipEventCreate(&f->t_ev[i]));
     }
-    const bhrt_frame_soa fields = device_fields(host, (int)method, dk != NULL);
+    const bhrt_frame_soa fields = device_fields(host, (int)method, dk != NULL, bh->spin != 0.0);
     for (int d = 0; d < ndev; d++) { /* device buffers: every chunk of device d */
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
@@ -1413,7 +1404,7 @@ int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
         jobs[d].c = c;
         jobs[d].n = m;
         if (ensure(&c->d_rays, &c->cap_rays, (size_t)m * sizeof(Ray), 0)) return -1;
-        if (device_soa(c, m, host, (int)method, dk != NULL, &jobs[d].dev)) return -1;
+        if (device_soa(c, m, host, (int)method, dk != NULL, bh->spin != 0.0, &jobs[d].dev)) return -1;
         HIP_TRY(hipMemcpyAsync(c->d_rays, rays + base[d], (size_t)m * sizeof(Ray),
                                hipMemcpyHostToDevice, c->stream));
         if (bhrt_trace_rays_device((const Ray*)c->d_rays, (int)m, bh, dk, cfg, method, flags,
@@ -1439,23 +1430,24 @@ int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
  * (raytracer.c:299-333, 728-753) */
 /* pack one traced range into the reference's RayTraceHit (fill_hit_info, raytracer.c:299-333,
  * and trace_ray's disk branch :728-753): only the fields the reference writes */
+static inline void pack_one(RayTraceHit* h, const bhrt_frame_soa* s, long i) {
+    h->result = (RayTraceResult)s->result[i];
+    h->steps = s->steps[i];
+    h->hit_position.x = s->hit_x[i];
+    h->hit_position.y = s->hit_y[i];
+    h->hit_position.z = s->hit_z[i];
+    h->distance = s->distance[i];
+    h->time_dilation = s->time_dilation[i];
+    if (h->result == RAY_MAX_DISTANCE) {
+        h->sky_direction.x = s->sky_x[i];
+        h->sky_direction.y = s->sky_y[i];
+        h->sky_direction.z = s->sky_z[i];
+    }
+}
+
 static void pack_hits(RayTraceHit* hits, long n, const bhrt_frame_soa* s, int nthreads) {
 #pragma omp parallel for schedule(static) num_threads(nthreads) if (n >= 65536)
-    for (long i = 0; i < n; i++) {
-        RayTraceHit* h = &hits[i];
-        h->result = (RayTraceResult)s->result[i];
-        h->steps = s->steps[i];
-        h->hit_position.x = s->hit_x[i];
-        h->hit_position.y = s->hit_y[i];
-        h->hit_position.z = s->hit_z[i];
-        h->distance = s->distance[i];
-        h->time_dilation = s->time_dilation[i];
-        if (h->result == RAY_MAX_DISTANCE) {
-            h->sky_direction.x = s->sky_x[i];
-            h->sky_direction.y = s->sky_y[i];
-            h->sky_direction.z = s->sky_z[i];
-        }
-    }
+    for (long i = 0; i < n; i++) pack_one(&hits[i], s, i);
 }
 
 /* the SoA fields a RayTraceHit needs, laid out consecutively from p for n rays */
@@ -1474,12 +1466,26 @@ static void hit_fields(char* p, long n, bhrt_frame_soa* s) {
 }
 #define HIT_BYTES (2 * sizeof(int32_t) + 8 * sizeof(double))
 
-/* Large batches: K contiguous chunks per device on alternating trace streams. Launching chunk
- * k first copies its rays into pinned staging (OpenMP threads; so the upload is asynchronous and
- * overlaps the chunks already tracing); each chunk's results come back on the copy stream, and
- * the host packs a chunk into hits[] as soon as it lands, with nthreads threads. The first chunk
- * is half the size of the others, so the GPU starts tracing after half a chunk's staging.
- * BHRT_HOST_TIMING=1 prints where a call's time went. */
+/* Large batches: K chunks per device on alternating trace streams. A device's rays are cut into
+ * blocks of BHRT_BATCH_BLOCK dealt round robin over the chunks (chunk k holds blocks k, k + K,
+ * ...), so every chunk carries the same mix of short and long rays whatever the order of the
+ * caller's array (row-major camera rays put the expensive rows in one contiguous quarter).
+ * Launching chunk k first copies its blocks into consecutive pinned staging (OpenMP threads;
+ * so the upload is asynchronous and overlaps the chunks already tracing); each chunk's results
+ * come back in one copy on the copy stream, and the host packs a chunk into hits[] as soon as
+ * it lands, with nthreads threads. BHRT_HOST_TIMING=1 prints where a call's time went. */
+#define BHRT_BATCH_BLOCK 1024L
+
+/* rays of chunk k when a device's m rays are dealt in blocks round robin over K chunks (only the
+ * device's last block can be partial) */
+static long batch_chunk_rays(long m, int K, int k) {
+    const long nb = (m + BHRT_BATCH_BLOCK - 1) / BHRT_BATCH_BLOCK;
+    if (k >= nb) return 0;
+    long cnt = ((nb - 1 - k) / K + 1) * BHRT_BATCH_BLOCK;
+    if ((nb - 1) % K == k) cnt -= nb * BHRT_BATCH_BLOCK - m;
+    return cnt;
+}
+
 static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* bh,
                                 const AccretionDiskParams* dk, const SimulationConfig* cfg,
                                 RayTraceHit* hits, int nthreads) {
@@ -1497,17 +1503,18 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
     const int timing = getenv("BHRT_HOST_TIMING") != NULL;
     struct timespec tt[4];
     clock_gettime(CLOCK_MONOTONIC, &tt[0]);
-    long base[BHRT_MAX_CHUNKS + 1][BHRT_MAX_DEV]; /* chunk k of device d: [base[k][d], base[k+1][d]) */
+    long d0s[BHRT_MAX_DEV], ms[BHRT_MAX_DEV];
+    long off[BHRT_MAX_CHUNKS + 1][BHRT_MAX_DEV]; /* chunk k of device d: staging [off[k], off[k+1]) */
     shard_job jobs[BHRT_MAX_CHUNKS][BHRT_MAX_DEV];
     for (int d = 0; d < ndev; d++) {
-        const long d0 = (long)n * d / ndev, d1 = (long)n * (d + 1) / ndev;
-        /* chunk boundaries in units of 1/(2K - 1): the first chunk one unit, the others two */
-        for (int k = 0; k <= K; k++)
-            base[k][d] = k == 0 ? d0 : d0 + (d1 - d0) * (2 * k - 1) / (2 * K - 1);
+        d0s[d] = (long)n * d / ndev;
+        ms[d] = (long)n * (d + 1) / ndev - d0s[d];
+        off[0][d] = 0;
+        for (int k = 0; k < K; k++) off[k + 1][d] = off[k][d] + batch_chunk_rays(ms[d], K, k);
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
         HIP_TRY(hipSetDevice(d));
-        const long m = d1 - d0;
+        const long m = ms[d];
         if (ensure(&c->d_rays, &c->cap_rays, (size_t)m * sizeof(Ray), 0) ||
             ensure(&c->d_soa, &c->cap_soa, (size_t)m * HIT_BYTES + 4096 * K, 0) ||
             ensure(&c->h_rays, &c->cap_hrays, (size_t)m * sizeof(Ray), 1) ||
@@ -1519,13 +1526,20 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
             devctx_t* c = ctx_get(d);
             hipStream_t st = (k & 1) ? c->stream2 : c->stream;
             HIP_TRY(hipSetDevice(d));
-            const long d0 = base[0][d], a = base[k][d] - d0, m = base[k + 1][d] - base[k][d];
+            const long a = off[k][d], m = off[k + 1][d] - a, md = ms[d];
             jobs[k][d].c = c;
             jobs[k][d].n = m;
             hit_fields((char*)c->d_soa + (size_t)a * HIT_BYTES + 256 * k, m, &jobs[k][d].dev);
             if (m > 0) {
                 Ray* hr = (Ray*)c->h_rays + a;
-                par_memcpy(hr, rays + base[k][d], (size_t)m * sizeof(Ray), stage_threads);
+                const Ray* src = rays + d0s[d];
+                const long nbk = (m + BHRT_BATCH_BLOCK - 1) / BHRT_BATCH_BLOCK;
+#pragma omp parallel for schedule(static) num_threads(stage_threads) if (nbk >= 4)
+                for (long j = 0; j < nbk; j++) { /* local block j = block k + j K of the device */
+                    const long b0 = (k + j * K) * BHRT_BATCH_BLOCK;
+                    const long len = md - b0 < BHRT_BATCH_BLOCK ? md - b0 : BHRT_BATCH_BLOCK;
+                    memcpy(hr + j * BHRT_BATCH_BLOCK, src + b0, (size_t)len * sizeof(Ray));
+                }
                 HIP_TRY(hipMemcpyAsync((Ray*)c->d_rays + a, hr, (size_t)m * sizeof(Ray),
                                        hipMemcpyHostToDevice, st));
                 if (bhrt_trace_rays_device((const Ray*)c->d_rays + a, (int)m, bh, dk, cfg,
@@ -1545,14 +1559,19 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
     for (int k = 0; k < K; k++)
         for (int d = 0; d < ndev; d++) {
             devctx_t* c = jobs[k][d].c;
-            const long a = base[k][d] - base[0][d], m = jobs[k][d].n;
+            const long a = off[k][d], m = jobs[k][d].n;
             HIP_TRY(hipSetDevice(d));
             clock_gettime(CLOCK_MONOTONIC, &tt[2]);
             HIP_TRY(hipEventSynchronize(c->chunk_copied[k]));
             bhrt_frame_soa s;
             hit_fields((char*)c->h_stage + (size_t)a * HIT_BYTES, m, &s);
             clock_gettime(CLOCK_MONOTONIC, &tt[3]);
-            pack_hits(hits + base[k][d], m, &s, nthreads);
+            RayTraceHit* h = hits + d0s[d];
+#pragma omp parallel for schedule(static) num_threads(nthreads) if (m >= 65536)
+            for (long i = 0; i < m; i++) { /* local ray i: block k + (i / B) K of the device */
+                const long j = i / BHRT_BATCH_BLOCK;
+                pack_one(&h[(k + j * K) * BHRT_BATCH_BLOCK + (i - j * BHRT_BATCH_BLOCK)], &s, i);
+            }
             if (timing) {
                 struct timespec t4;
                 clock_gettime(CLOCK_MONOTONIC, &t4);

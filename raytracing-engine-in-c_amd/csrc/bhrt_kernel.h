@@ -75,10 +75,13 @@ typedef struct {
 
 /* Whether the trace kernel writes a scene's colour outputs at each ray's exit (no separate
  * colour pass re-reading the hits): RKF45 scenes with a disk (C3: rays end after ~2 attempts,
- * so the pass is a large share of the frame; +5% same-box). Elsewhere the separate pass runs
- * on the other stream's tail and costs less than the colour code's registers in the trace
- * loop (C4 -3.5%, C2/C5 neutral; profiles/r03_ab_kernel.txt). */
-#define BHRT_COLOUR_IN_TRACE(method, has_disk) ((method) == INTEGRATOR_RKF45 && (has_disk))
+ * so the pass is a large share of the frame; +5% same-box) and, since round 4, RK4 scenes with
+ * a disk at spin != 0 (C4: the pass and its dispatch are a fixed cost per frame that a
+ * strong-scaled shard cannot hide). Elsewhere (C2) the separate pass runs on the other
+ * stream's tail and costs less than the colour code's registers in the trace loop
+ * (profiles/r03_ab/fused_colour_rk4.txt). */
+#define BHRT_COLOUR_IN_TRACE(method, has_disk, spin) \
+    ((has_disk) && ((method) == INTEGRATOR_RKF45 || ((method) == INTEGRATOR_RK4 && (spin))))
 
 typedef struct {
     bhrt_scene_k sc;
@@ -105,6 +108,8 @@ typedef struct {
                              of each ray at its exit; else a separate colour pass runs */
     const int* order;     /* camera frames: the claim order, queue position -> ray id (a
                              permutation of [0, n)); NULL = ray id order */
+    int skip_redo;        /* the redo launch may be left out where no ray can be evicted
+                             (geodesic.hip launch_trace_pair); BHRT_SKIP_REDO=0: always launch */
 } bhrt_kparams;
 
 /* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and

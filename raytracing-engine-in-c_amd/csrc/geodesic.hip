@@ -1144,6 +1144,10 @@ __device__ __forceinline__ unsigned to_u8(float v) {
 __device__ __forceinline__ void colour_of(const Scene& sc, int res, double hx, double hy,
                                           double dx, double dy, double dz, double& r,
                                           double& g, double& b) {
+    // no FP contraction here: the colour is then the same IEEE operation sequence wherever it
+    // is inlined (the trace kernel's exit or the separate k_colour pass), so both colour paths
+    // give the same bits (test_display_path_rgba), as the reference's own non-FMA build does
+#pragma clang fp contract(off)
     if (res == RAY_DISK) {
         const double rxy = sqrt(hx * hx + hy * hy);  // raytracer.c:201-228
         double nr = (rxy - sc.disk_in) / (sc.disk_out - sc.disk_in);
@@ -1237,10 +1241,10 @@ __device__ __forceinline__ const bhrt_kparams& cold(const bhrt_kparams&) {
     return *(const bhrt_kparams*)p;
 }
 
-template <int METHOD, bool DISK>
+template <int METHOD, bool DISK, bool SPIN0>
 __device__ __forceinline__ void store_ray(const bhrt_kparams& kp, int i, const Ray_& R, int term) {
     store_hit(kp.out, i, R, term, kp.sc);
-    if (!BHRT_COLOUR_IN_TRACE(METHOD, DISK)) return;
+    if (!BHRT_COLOUR_IN_TRACE(METHOD, DISK, !SPIN0)) return;
     if (kp.colour_fused && (kp.out.rgb_r || kp.out.rgba32f || kp.out.rgba8)) {
         const int res = term == T_DISK ? RAY_DISK : (term == T_HORIZON ? RAY_HORIZON : RAY_MAX_STEPS);
         double r, g, b;
@@ -1539,7 +1543,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     n.rays++;
                     live = true;
                     if (kp.sc.max_steps <= 0) {  // loop never runs: MAX_STEPS, steps 0
-                        store_ray<METHOD, DISK>(kc, rid, R, T_MAXSTEPS);
+                        store_ray<METHOD, DISK, SPIN0>(kc, rid, R, T_MAXSTEPS);
                         live = false;
                         n.huge = false;
                     }
@@ -1580,7 +1584,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 kp.redo[atomicAdd(kp.ctl + 6, 1ull)] = rid;
                 live = false;
             } else if (term != T_NONE) {
-                store_ray<METHOD, DISK>(kc, rid, R, term);
+                store_ray<METHOD, DISK, SPIN0>(kc, rid, R, term);
                 live = false;
             }
         }
@@ -1754,6 +1758,14 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     bhrt_kparams k = kp;
     k.claim_shift = claim_shift(blocks, kp.claim_div, kp.queue_bits);
     k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, 256, 0, st>>>(k);
+    // A camera launch on the zero-acceleration paths (C4, C5) evicts no ray: its loop has no
+    // sincos that can raise the large-argument flag (rotation_trig), and the one refill-time
+    // test, |state[5]| < rot_vmax, holds for every camera ray (|state[5]| = |v_r| is a dot
+    // product of two unit vectors, <= 1 + 2^-50, checked against rot_vmax here) -- so no redo
+    // launch follows, one dispatch less per frame (what a strong-scaled shard pays for)
+    if (rotation_trig<METHOD, SPIN0, FAR, false>() && kp.src == BHRT_SRC_CAMERA &&
+        kp.sc.rot_vmax > 1.001 && kp.skip_redo)
+        return;
     // rays evicted by the large-argument check (normally none: every wave exits at once). 64
     // workgroups: the evicted rays are rare, and a full-chip grid of waves that only read the
     // count and exit costs ~15 us per frame (C3 +8.5% same-box, profiles/r02_ab_v24.txt)

@@ -539,12 +539,14 @@ def _display_u8(v):
         return (np.trunc(m * np.float32(255.0)).astype(np.int64) & 0xFF).astype(np.uint8)
 
 
-@pytest.mark.parametrize("cname,fuse", [("C2", "1"), ("C4", "1"), ("C3", "1"), ("C3", "0")])
+@pytest.mark.parametrize("cname,fuse", [("C2", "1"), ("C4", "1"), ("C4", "0"), ("C3", "1"),
+                                        ("C3", "0")])
 def test_display_path_rgba(bhrt_lib, oracle, monkeypatch, cname, fuse):
     """the visualizer's texture buffer (float RGBA with alpha 1, then
     RGBA8 by its own conversion) produced by the colour pass, row 0 = top. C3 (RKF45 with a
-    disk) writes the colour in the trace kernel (BHRT_FUSE_COLOUR, default on):
-    both forms are run, and must give the same buffers."""
+    disk) and C4 (RK4 Kerr with a disk) write the colour in the trace kernel
+    (BHRT_FUSE_COLOUR, default on): both forms are run, and must give the same
+    buffers bit for bit (colour_of is compiled without FP contraction in both)."""
     monkeypatch.setenv("BHRT_FUSE_COLOUR", fuse)
     c = configs.CONFIGS[cname]
     bh, dk, cfg = c.scene()
@@ -552,7 +554,7 @@ def test_display_path_rgba(bhrt_lib, oracle, monkeypatch, cname, fuse):
     W, H = 96, 54
     fields = abi.SOA_FIELDS + abi.DISPLAY_FIELDS
     got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags, fields=fields)
-    if cname == "C3":  # the other colour form gives every output bit for bit
+    if cname in ("C3", "C4"):  # the other colour form gives every output bit for bit
         monkeypatch.setenv("BHRT_FUSE_COLOUR", "0" if fuse == "1" else "1")
         other = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags, fields=fields)
         other_only = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags,
