@@ -45,4 +45,7 @@ if [ -z "$SKIP_PLAN" ]; then
     || { echo "plan shards failed"; tail -20 $OUT/plan_shards.err; exit 1; }
   python tools/plan_summary.py $OUT/plan_shards.jsonl --out $OUT/plan_summary.txt
 fi
+if [ -n "${PMC_CFGS-C4 C5}" ]; then
+  echo "== pmc" && CONFIGS="${PMC_CFGS-C4 C5}" bash tools/pmc_all.sh || exit 1
+fi
 echo all-done
