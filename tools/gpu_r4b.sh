@@ -16,11 +16,11 @@ if [ -z "$SKIP_TESTS" ]; then
   grep -E "FAILED|ERROR" $OUT/pytest_gpu.log | head -20
   [ $rc -le 1 ] || { echo "pytest rc=$rc: stopping"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 fi
-KNOBS=${KNOBS:-"base base:BHRT_FUSE_COLOUR=0 base:BHRT_SKIP_REDO=0 base:BHRT_CLAIM_DIV=2 base:BHRT_CLAIM_DIV=4"}
+KNOBS=${KNOBS:-"base base:BHRT_FUSE_COLOUR=0 base:BHRT_SKIP_REDO=0 base:BHRT_CLAIM_DIV=0 base:BHRT_CLAIM_DIV=4"}
 if [ -z "$SKIP_AB" ]; then
   echo "== ab C4" && CFG=C4 VARIANTS="$KNOBS" ROUNDS=${AB_ROUNDS:-3} EXTRA="--no-host-path" bash tools/ab.sh || exit 1
   echo "== ab C4 plan-8 shard 0" && CFG=C4 VARIANTS="$KNOBS" ROUNDS=${AB_ROUNDS:-3} EXTRA="--no-host-path --plan-gpus 8 --shard 0" bash tools/ab.sh || exit 1
-  echo "== ab C5" && CFG=C5 VARIANTS="base base:BHRT_CLAIM_DIV=2 base:BHRT_CLAIM_DIV=4 base:BHRT_SKIP_REDO=0" ROUNDS=${AB_ROUNDS:-3} EXTRA="--no-host-path" bash tools/ab.sh || exit 1
+  echo "== ab C5" && CFG=C5 VARIANTS="base base:BHRT_CLAIM_DIV=0 base:BHRT_CLAIM_DIV=4 base:BHRT_SKIP_REDO=0" ROUNDS=${AB_ROUNDS:-3} EXTRA="--no-host-path" bash tools/ab.sh || exit 1
 fi
 for v in ${TRACE_VARIANTS-p8s1 p8s2}; do
   case $v in
