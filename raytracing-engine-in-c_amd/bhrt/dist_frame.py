@@ -278,10 +278,16 @@ class FramePipeline:
         for f in self.gather:
             a, b = fb.offsets[f]
             inner = self._inner(f)
-            src = src_all[:, a - a0:b - a0].view(fb.views[f].dtype).view(world, nbk, B, W,
-                                                                          *inner)
             dst = self.images[slot][f]
-            dst.view(nbk, S, B, W, *inner)[:, self.first:self.first + world].copy_(
-                src.transpose(0, 1))
+            raw = src_all[:, a - a0:b - a0]
+            if fb.views[f].dtype == torch.uint8 and inner == (4,):
+                # rgba8: one 4-byte word per pixel -- an int32 copy moves 4x fewer elements
+                # than a uint8 one (an 8-shard C4 frame: ~8x faster on rank 0)
+                src = raw.view(torch.int32).view(world, nbk, B, W)
+                d = dst.view(torch.int32).view(nbk, S, B, W)
+            else:
+                src = raw.view(fb.views[f].dtype).view(world, nbk, B, W, *inner)
+                d = dst.view(nbk, S, B, W, *inner)
+            d[:, self.first:self.first + world].copy_(src.transpose(0, 1))
             image[f] = dst[:H]
         return Assembled(image, local, idx)

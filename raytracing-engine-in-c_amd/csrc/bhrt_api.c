@@ -683,6 +683,24 @@ static void claim_tiles(bhrt_camera_k* k, int W, int nrows) {
             k->tile_h_log2 = shape[i][1];
             k->tiles_per_row = W / tw;
             k->inv_tiles_per_row = 1.0 / (double)k->tiles_per_row;
+            k->ntiles = k->tiles_per_row * (nrows / th);
+            k->tile_stride = 0;
+            if (env_int("BHRT_TILE_SCATTER", 0) && k->ntiles > 2) {
+                /* a stride near ntiles / golden ratio, coprime with ntiles: consecutive claims
+                 * (a wave's block of tiles) land far apart in the image */
+                int st = (int)(k->ntiles * 0.6180339887498949);
+                while (st > 1) {
+                    int a = st, b = k->ntiles;
+                    while (b) {
+                        const int t = a % b;
+                        a = b;
+                        b = t;
+                    }
+                    if (a == 1) break;
+                    st--;
+                }
+                k->tile_stride = st;
+            }
             return;
         }
     }

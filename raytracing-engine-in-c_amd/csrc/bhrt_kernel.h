@@ -71,6 +71,8 @@ typedef struct {
      * (one wavefront), tiles row-major; tiles_per_row == 0: ray id order */
     int tile_w_log2, tile_h_log2, tiles_per_row;
     double inv_tiles_per_row;        /* RN(1 / tiles_per_row)                   */
+    int ntiles, tile_stride;         /* tile_stride > 0: the claim order visits tile
+                                        (t * tile_stride) mod ntiles at step t (scatter) */
 } bhrt_camera_k;
 
 /* Whether the trace kernel writes a scene's colour outputs at each ray's exit (no separate

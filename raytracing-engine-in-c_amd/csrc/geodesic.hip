@@ -1270,7 +1270,10 @@ __device__ __forceinline__ int claim_ray(const bhrt_kparams& kp, int qpos) {
     if (kp.order) return kp.order[qpos];
     const bhrt_camera_k& cm = kp.cam;
     if (cm.tiles_per_row == 0) return qpos;
-    const int t = qpos >> 6, w = qpos & 63;
+    int t = qpos >> 6;
+    const int w = qpos & 63;
+    if (cm.tile_stride > 0)
+        t = (int)(((unsigned long long)(unsigned)t * (unsigned)cm.tile_stride) % (unsigned)cm.ntiles);
     const int trow = div_floor(t, cm.tiles_per_row, cm.inv_tiles_per_row);
     const int tcol = t - trow * cm.tiles_per_row;
     const int prow = (trow << cm.tile_h_log2) + (w >> cm.tile_w_log2);

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-4 session C: same-box A/B of claim-schedule knobs on C4 (whole frame and one shard of
+# the 8-GPU plan) and C5, then the C4 plan shards with the chosen defaults.
+set -o pipefail
+cd "$(dirname "$0")/.."
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+KNOBS=${KNOBS:-"base base:BHRT_TILE_SCATTER=1 base:BHRT_REFILL=32 base:BHRT_REFILL=48 base:BHRT_QUEUES=4 base:BHRT_QUEUES=32 base:BHRT_CLAIM_MIN=128"}
+echo "== ab C4 plan-8 shard 0" && CFG=C4 VARIANTS="$KNOBS" ROUNDS=${AB_ROUNDS:-2} EXTRA="--no-host-path --plan-gpus 8 --shard 0" bash tools/ab.sh || exit 1
+echo "== ab C4" && CFG=C4 VARIANTS="$KNOBS" ROUNDS=${AB_ROUNDS:-2} EXTRA="--no-host-path" bash tools/ab.sh || exit 1
+[ -z "$C5_KNOBS" ] || { echo "== ab C5" && CFG=C5 VARIANTS="$C5_KNOBS" ROUNDS=${AB_ROUNDS:-2} EXTRA="--no-host-path" bash tools/ab.sh || exit 1; }
+if [ -z "$SKIP_PLAN" ]; then
+  echo "== plan shards"
+  CONFIGS="${PLAN_CFGS:-C4}" bash tools/plan_shards.sh > $OUT/plan_shards.jsonl 2> $OUT/plan_shards.err \
+    || { echo "plan shards failed"; tail -20 $OUT/plan_shards.err; exit 1; }
+  python tools/plan_summary.py $OUT/plan_shards.jsonl --out $OUT/plan_summary.txt
+fi
+echo all-done
