@@ -336,7 +336,8 @@ def test_refill_threshold_does_not_change_results(bhrt_lib, cname):
 def test_claim_order_does_not_change_results(bhrt_lib, monkeypatch, cname):
     """bhrt_set_claim_order (the queue position -> ray id permutation of device camera frames)
     is a speed knob only: the default tiled order (64-pixel tiles, geodesic.hip claim_ray), ray
-    id order (BHRT_TILES=0), a random permutation and the reversed order give the same frame
+    id order (BHRT_TILES=0), scattered tiles (BHRT_TILE_SCATTER=1), a random permutation and
+    the reversed order give the same frame
     bit for bit, on the in-kernel set-up paths (C2-C5) and the k_init table path (C1); a
     permutation of another length is ignored."""
     import torch
@@ -350,14 +351,18 @@ def test_claim_order_does_not_change_results(bhrt_lib, monkeypatch, cname):
               torch.arange(n - 1, -1, -1, dtype=torch.int32, device="cuda"),
               torch.arange(n + 64, dtype=torch.int32, device="cuda")]  # wrong length: ignored
     orders.insert(1, "ids")
+    orders.insert(2, "scatter")
     outs = []
     try:
         for order in orders:
-            if isinstance(order, str):  # ray id order instead of the default tiles
+            monkeypatch.delenv("BHRT_TILES", raising=False)
+            monkeypatch.delenv("BHRT_TILE_SCATTER", raising=False)
+            if isinstance(order, str) and order == "ids":  # ray id order, not the default tiles
                 monkeypatch.setenv("BHRT_TILES", "0")
                 order = None
-            else:
-                monkeypatch.delenv("BHRT_TILES", raising=False)
+            elif isinstance(order, str):  # "scatter": the tiles visited with a coprime stride
+                monkeypatch.setenv("BHRT_TILE_SCATTER", "1")
+                order = None
             bhrt_lib.set_claim_order(order.data_ptr() if order is not None else None,
                                      order.numel() if order is not None else 0)
             t = {f: torch.full((n,), -1, dtype=torch.int32 if f in ("result", "steps")
