@@ -259,6 +259,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_issue = time.perf_counter() - t0  # host time to issue the K frames (no GPU wait)
     frame = pipe.finish()
     torch.cuda.synchronize()
     if world > 1:
@@ -344,6 +345,7 @@ def main():
             "event_avg_ms": round(kern_ms, 4),
             "streams": len(streams),
             "iterations_per_launch": st["iterations"] / max(st["launches"], 1),
+            "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 4),
             "mean_iterations_per_ray": st["iterations"] / max(st["rays"], 1),
         },
         "roofline": {

@@ -111,8 +111,11 @@ class FrameBuffer:
         return rng[0][0], rng[-1][1]
 
     def soa(self):
-        from . import lib
-        return lib.soa_from_tensors(self.views)
+        """The FrameSoA of this buffer (built once: the pointers never change)."""
+        if getattr(self, "_soa", None) is None:
+            from . import lib
+            self._soa = lib.soa_from_tensors(self.views)
+        return self._soa
 
 
 def sample_offset(k):
@@ -244,6 +247,44 @@ class FramePipeline:
         if self.rank == 0:
             self.last = self._assemble(slot)
 
+    # Per-frame host work is a handful of tensor ops: every view the assembly needs is built
+    # once per slot (a C4 shard of an 8-GPU plan renders in ~0.1 ms, so per-frame Python
+    # view-building, ~0.1-0.2 ms, had become the frame rate's bound)
+    def _plan(self, slot):
+        plans = self.__dict__.setdefault("_plans", {})
+        if slot in plans:
+            return plans[slot]
+        fb, H, W, world = self.bufs[slot], self.H, self.W, self.world
+        local, idx = self._local(fb)
+        copies, image = [], {}
+        if self.mode == "samples":
+            if world == 1:
+                image = {f: local[f] for f in self.gather}
+        elif self.direct:
+            image = {f: local[f] for f in self.gather}
+        else:
+            B, S = self.row_block, self.shards
+            nbk = fb.n // W // B                       # blocks per (padded) shard
+            src_all = self.gathered[slot]
+            a0 = self.span[0]
+            for f in self.gather:
+                a, b = fb.offsets[f]
+                inner = self._inner(f)
+                dst = self.images[slot][f]
+                raw = src_all[:, a - a0:b - a0]
+                if fb.views[f].dtype == torch.uint8 and inner == (4,):
+                    # rgba8: one 4-byte word per pixel -- an int32 copy moves 4x fewer
+                    # elements than a uint8 one (an 8-shard C4 frame: ~8x faster on rank 0)
+                    src = raw.view(torch.int32).view(world, nbk, B, W)
+                    d = dst.view(torch.int32).view(nbk, S, B, W)
+                else:
+                    src = raw.view(fb.views[f].dtype).view(world, nbk, B, W, *inner)
+                    d = dst.view(nbk, S, B, W, *inner)
+                copies.append((d[:, self.first:self.first + world], src.transpose(0, 1)))
+                image[f] = dst[:H]
+        plans[slot] = (local, idx, copies, image)
+        return plans[slot]
+
     def _local(self, fb):
         if self.mode == "samples":
             return ({f: fb.views[f].view(self.H, self.W, *self._inner(f)) for f in fb.fields},
@@ -259,35 +300,10 @@ class FramePipeline:
         return (k,) if k > 1 else ()
 
     def _assemble(self, slot):
-        fb, H, W, world = self.bufs[slot], self.H, self.W, self.world
-        local, idx = self._local(fb)
-        if self.mode == "samples":
-            if world == 1:
-                image = {f: local[f] for f in self.gather}
-            else:
-                image = {f: (self.colour[slot][i] / world).view(H, W)
-                         for i, f in enumerate(self.gather)}
-            return Assembled(image, local, idx)
-        if self.direct:
-            return Assembled({f: local[f] for f in self.gather}, local, idx)
-        B, S = self.row_block, self.shards
-        nbk = fb.n // W // B                       # blocks per (padded) shard
-        src_all = self.gathered[slot]
-        a0 = self.span[0]
-        image = {}
-        for f in self.gather:
-            a, b = fb.offsets[f]
-            inner = self._inner(f)
-            dst = self.images[slot][f]
-            raw = src_all[:, a - a0:b - a0]
-            if fb.views[f].dtype == torch.uint8 and inner == (4,):
-                # rgba8: one 4-byte word per pixel -- an int32 copy moves 4x fewer elements
-                # than a uint8 one (an 8-shard C4 frame: ~8x faster on rank 0)
-                src = raw.view(torch.int32).view(world, nbk, B, W)
-                d = dst.view(torch.int32).view(nbk, S, B, W)
-            else:
-                src = raw.view(fb.views[f].dtype).view(world, nbk, B, W, *inner)
-                d = dst.view(nbk, S, B, W, *inner)
-            d[:, self.first:self.first + world].copy_(src.transpose(0, 1))
-            image[f] = dst[:H]
+        local, idx, copies, image = self._plan(slot)
+        if self.mode == "samples" and self.world > 1:
+            image = {f: (self.colour[slot][i] / self.world).view(self.H, self.W)
+                     for i, f in enumerate(self.gather)}
+        for d, src in copies:
+            d.copy_(src)
         return Assembled(image, local, idx)
