@@ -114,8 +114,9 @@ def parse():
                    help="skip the host-buffer leg (its chunked launches would mix into a "
                         "profiler's per-launch kernel averages)")
     p.add_argument("--streams", type=int, default=2,
-                   help="consecutive frames alternate between this many HIP streams, so the "
-                        "next frame's rays fill the CUs the tail of the current frame frees")
+                   help="consecutive frames alternate between this many HIP streams (1-4; "
+                        "one frame buffer each), so the next frames' rays fill the CUs the tail "
+                        "of the current frame frees")
     p.add_argument("--weak-mode", choices=("tiles", "samples"), default="tiles",
                    help="weak configs at N GPUs: tiles = N shards of a frame (default); "
                         "samples = N sub-pixel sample planes of the configuration frame "
@@ -171,8 +172,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.streams not in (1, 2):  # FramePipeline has two buffer slots, one per stream
-        raise SystemExit("--streams must be 1 or 2")
+    if not 1 <= args.streams <= 4:  # FramePipeline keeps one buffer slot per stream
+        raise SystemExit("--streams must be 1..4")
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # rehearsal of the N-GPU path on a one-GPU box: every rank on GPU 0, gloo collectives
@@ -230,7 +231,8 @@ def main():
     gather = {"all": None, "image": RGB_FIELDS, "rgba8": DISPLAY_FIELD}[args.gather]
     fields = FIELDS + DISPLAY_FIELD if args.gather == "rgba8" else FIELDS
     pipe = FramePipeline(n, device, world, rank, "samples" if samples else "shards", H, W, B,
-                         fields, shards=S, gather=gather, first_shard=shard - rank)
+                         fields, shards=S, gather=gather, first_shard=shard - rank,
+                         slots=args.streams)
     streams = ([torch.cuda.current_stream()] if args.streams <= 1 else
                [torch.cuda.Stream(device) for _ in range(args.streams)])
     frame_no = [0]
@@ -239,7 +241,8 @@ def main():
         # Frame k renders on streams[k % S]. A persistent k_trace launch ends with a tail in
         # which its last (up to max_steps-iteration) rays drain and CUs fall idle; with S > 1
         # the next frame's workgroups take those CUs (tools/wave_tail.py measures the tail).
-        # A frame buffer slot is reused two frames later, on the same stream when S = 2.
+        # A frame buffer slot is reused `streams` frames later (two with one stream), on the
+        # same stream.
         s = streams[frame_no[0] % len(streams)]
         frame_no[0] += 1
         with torch.cuda.stream(s):

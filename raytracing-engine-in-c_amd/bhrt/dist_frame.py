@@ -155,21 +155,23 @@ class FramePipeline:
     """
 
     def __init__(self, n, device, world, rank, mode, H, W, row_block=8,
-                 fields=abi.SOA_FIELDS, shards=None, gather=RGB_FIELDS, first_shard=0):
+                 fields=abi.SOA_FIELDS, shards=None, gather=RGB_FIELDS, first_shard=0,
+                 slots=2):
         assert mode in ("shards", "samples")
+        self.nslots = max(2, int(slots))  # frames in flight: a slot is reused nslots frames later
         self.world, self.rank, self.mode = world, rank, mode
         self.H, self.W, self.row_block = H, W, row_block
         self.shards = (shards or world) if mode == "shards" else 1
         self.first = first_shard  # rank r renders shard first_shard + r
         if mode == "shards" and not 0 <= first_shard <= self.shards - world:
             raise ValueError(f"{world} ranks from shard {first_shard} but {self.shards} shards")
-        self.bufs = [FrameBuffer(n, device, fields) for _ in range(2)]
+        self.bufs = [FrameBuffer(n, device, fields) for _ in range(self.nslots)]
         fb = self.bufs[0]
         self.gather = tuple(gather) if gather is not None else fb.fields
         self.span = fb.span(self.gather)
         if mode == "samples" and world > 1 and not set(self.gather) <= set(RGB_FIELDS):
             raise ValueError("samples mode reduces the colour planes only")
-        self.works = [None, None]
+        self.works = [None] * self.nslots
         self.frames = 0
         self.last = None
         self.images = self.gathered = self.colour = None
@@ -177,18 +179,18 @@ class FramePipeline:
         if mode == "samples":
             if world > 1:  # per slot: the colour planes summed over ranks (in place on rank 0)
                 self.colour = [torch.empty(len(self.gather), n, dtype=torch.float64,
-                                           device=device) for _ in range(2)]
+                                           device=device) for _ in range(self.nslots)]
             return
         self.direct = world == 1 and self.shards == 1  # the buffer IS the image
         if rank == 0 and not self.direct:
             a, b = self.span
             # one [world, bytes] receive tensor per slot; gather writes rank k's range to row k
             self.gathered = [torch.empty(world, b - a, dtype=torch.uint8, device=device)
-                             for _ in range(2)]
+                             for _ in range(self.nslots)]
             rows = padded_shard_rows(H, row_block, self.shards) * self.shards
             self.images = [{f: torch.zeros(rows, W, *self._inner(f), dtype=fb.views[f].dtype,
                                         device=device)
-                            for f in self.gather} for _ in range(2)]
+                            for f in self.gather} for _ in range(self.nslots)]
         # gloo gathers host tensors only: with device buffers (the one-GPU rehearsal of the
         # N-rank bench, BHRT_BENCH_SHARE_DEVICE) the gathered range travels through host
         # copies; RCCL gathers the device buffers directly
@@ -196,17 +198,17 @@ class FramePipeline:
                        dist.get_backend() == "gloo")
         if self.staged:
             a, b = self.span
-            self.host_send = [torch.empty(b - a, dtype=torch.uint8) for _ in range(2)]
-            self.host_recv = ([torch.empty(world, b - a, dtype=torch.uint8) for _ in range(2)]
-                              if rank == 0 else None)
+            self.host_send = [torch.empty(b - a, dtype=torch.uint8) for _ in range(self.nslots)]
+            self.host_recv = ([torch.empty(world, b - a, dtype=torch.uint8)
+                               for _ in range(self.nslots)] if rank == 0 else None)
 
     def next_buffer(self):
-        slot = self.frames % 2
+        slot = self.frames % self.nslots
         self._complete(slot)
         return self.bufs[slot]
 
     def submit(self):
-        slot = self.frames % 2
+        slot = self.frames % self.nslots
         fb = self.bufs[slot]
         a, b = self.span
         if self.mode == "samples":
@@ -231,8 +233,8 @@ class FramePipeline:
         self.frames += 1
 
     def finish(self):
-        for k in range(max(self.frames - 2, 0), self.frames):  # oldest first
-            self._complete(k % 2)
+        for k in range(max(self.frames - self.nslots, 0), self.frames):  # oldest first
+            self._complete(k % self.nslots)
         return self.last
 
     def _complete(self, slot):

@@ -10,6 +10,13 @@ KNOBS=${KNOBS:-"base base:BHRT_TILE_SCATTER=1 base:BHRT_REFILL=32 base:BHRT_REFI
 echo "== ab C4 plan-8 shard 0" && CFG=C4 VARIANTS="$KNOBS" ROUNDS=${AB_ROUNDS:-2} EXTRA="--no-host-path --plan-gpus 8 --shard 0" bash tools/ab.sh || exit 1
 echo "== ab C4" && CFG=C4 VARIANTS="$KNOBS" ROUNDS=${AB_ROUNDS:-2} EXTRA="--no-host-path" bash tools/ab.sh || exit 1
 [ -z "$C5_KNOBS" ] || { echo "== ab C5" && CFG=C5 VARIANTS="$C5_KNOBS" ROUNDS=${AB_ROUNDS:-2} EXTRA="--no-host-path" bash tools/ab.sh || exit 1; }
+for st in ${STREAM_SWEEP-2 3 4}; do  # frames in flight on a C4 plan shard and the whole C4 frame
+  for ex in "--plan-gpus 8 --shard 0" ""; do
+    timeout -k 10 120 python bench.py --config C4 --steps 40 --warmup 4 --no-cpu-baseline --no-host-path --streams $st $ex > $OUT/c4_streams.json 2>/dev/null \
+      || { echo "streams $st failed"; exit 1; }
+    python3 -c "import json; d=json.load(open('$OUT/c4_streams.json')); print('C4 streams $st', '$ex', d['value'], d['ms_per_step'], 'host', d['kernel']['host_issue_ms_per_step'])"
+  done
+done
 if [ -z "$SKIP_PLAN" ]; then
   echo "== plan shards"
   CONFIGS="${PLAN_CFGS:-C4}" bash tools/plan_shards.sh > $OUT/plan_shards.jsonl 2> $OUT/plan_shards.err \
