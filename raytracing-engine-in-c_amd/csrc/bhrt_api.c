@@ -98,7 +98,7 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 #define BHRT_QHEAD_OFF 32 /* u64 words */
 #define BHRT_SLOT_WORDS (BHRT_QHEAD_OFF + BHRT_QWORDS)
 #define BHRT_MAX_CHUNKS 8   /* host-buffer frames: pipelined chunks per device            */
-#define BHRT_SCRATCH_SLOTS 4
+#define BHRT_SCRATCH_SLOTS 8
 #define BHRT_FRAME_SLOTS 3  /* host-buffer frames in flight per thread (bhrt_render_frame_async) */
 #define BHRT_COPY_PARTS 4   /* host-buffer frames: a chunk's D2H in parts, each un-permuted as it lands */
 #define BHRT_NFIELDS 15
@@ -135,6 +135,7 @@ typedef struct {
     /* host-buffer frames (bhrt_render_frame): two trace streams for overlapping chunks, a
      * copy stream, and per chunk: trace finished / its D2H landed */
     hipStream_t stream2, copy;
+    hipStream_t xs[2]; /* trace streams 3 and 4 of pipelined ray batches (created on first use) */
     hipEvent_t chunk_done[BHRT_MAX_CHUNKS], chunk_copied[BHRT_MAX_CHUNKS];
     /* per frame slot of bhrt_render_frame_async: device SoA of every chunk, pinned staging
      * of the caller's fields, chunk traced / chunk copied */
@@ -1138,6 +1139,8 @@ static void drain_devices(int ndev) {
         if (!c || hipSetDevice(d) != hipSuccess) continue;
         (void)hipStreamSynchronize(c->stream);
         (void)hipStreamSynchronize(c->stream2);
+        for (int i = 0; i < 2; i++)
+            if (c->xs[i]) (void)hipStreamSynchronize(c->xs[i]);
         (void)hipStreamSynchronize(c->copy);
     }
     memcpy(g_err, err, sizeof err);
@@ -1519,6 +1522,12 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
     if (env && atoi(env) >= 1 && atoi(env) <= BHRT_MAX_CHUNKS) K = atoi(env);
     const int stage_threads = host_threads();
     const int timing = getenv("BHRT_HOST_TIMING") != NULL;
+    /* trace streams the chunks rotate over: with 2, chunk k + 2 cannot start before chunk k
+     * has drained (stream order), so two chunk tails can stall the pipeline; with up to 4
+     * every chunk is queued at once and the GPU takes their workgroups as CUs free up */
+    int nst = env_int("BHRT_BATCH_STREAMS", 4);
+    if (nst < 1) nst = 1;
+    if (nst > 4) nst = 4;
     struct timespec tt[4];
     clock_gettime(CLOCK_MONOTONIC, &tt[0]);
     long d0s[BHRT_MAX_DEV], ms[BHRT_MAX_DEV];
@@ -1532,6 +1541,8 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
         HIP_TRY(hipSetDevice(d));
+        for (int i = 0; i + 2 < nst; i++)
+            if (!c->xs[i]) HIP_TRY(hipStreamCreateWithFlags(&c->xs[i], hipStreamNonBlocking));
         const long m = ms[d];
         if (ensure(&c->d_rays, &c->cap_rays, (size_t)m * sizeof(Ray), 0) ||
             ensure(&c->d_soa, &c->cap_soa, (size_t)m * HIT_BYTES + 4096 * K, 0) ||
@@ -1542,7 +1553,8 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
     for (int k = 0; k < K; k++)
         for (int d = 0; d < ndev; d++) {
             devctx_t* c = ctx_get(d);
-            hipStream_t st = (k & 1) ? c->stream2 : c->stream;
+            const int si = k % nst;
+            hipStream_t st = si == 0 ? c->stream : si == 1 ? c->stream2 : c->xs[si - 2];
             HIP_TRY(hipSetDevice(d));
             const long a = off[k][d], m = off[k + 1][d] - a, md = ms[d];
             jobs[k][d].c = c;

@@ -17,6 +17,14 @@ for st in ${STREAM_SWEEP-2 3 4}; do  # frames in flight on a C4 plan shard and t
     python3 -c "import json; d=json.load(open('$OUT/c4_streams.json')); print('C4 streams $st', '$ex', d['value'], d['ms_per_step'], 'host', d['kernel']['host_issue_ms_per_step'])"
   done
 done
+if [ -z "$SKIP_BATCH" ]; then
+  for bs in 4 2; do
+    echo "== batch probe, $bs trace streams"
+    CHUNKS="4 6 8" BHRT_BATCH_STREAMS=$bs BHRT_HOST_TIMING=1 timeout -k 10 300 python tools/batch_probe.py > $OUT/batch_probe_s$bs.txt 2> $OUT/batch_probe_s$bs.err \
+      || { echo "batch probe failed"; tail -20 $OUT/batch_probe_s$bs.err; exit 1; }
+    cat $OUT/batch_probe_s$bs.txt
+  done
+fi
 if [ -z "$SKIP_PLAN" ]; then
   echo "== plan shards"
   CONFIGS="${PLAN_CFGS:-C4}" bash tools/plan_shards.sh > $OUT/plan_shards.jsonl 2> $OUT/plan_shards.err \
