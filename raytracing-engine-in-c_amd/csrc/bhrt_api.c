@@ -524,6 +524,7 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
     claim_policy(kp);
     kp->colour_fused = colour_fused((int)method, dk != NULL, bh->spin != 0.0);
     kp->skip_redo = env_int("BHRT_SKIP_REDO", 1) != 0;
+    kp->block_lanes = env_int("BHRT_TRACE_BLOCK", 256);
     kp->cam.rows.row_block = 1;
     kp->cam.rows.num_shards = 1;
     return 0;
@@ -1522,10 +1523,9 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
     if (env && atoi(env) >= 1 && atoi(env) <= BHRT_MAX_CHUNKS) K = atoi(env);
     const int stage_threads = host_threads();
     const int timing = getenv("BHRT_HOST_TIMING") != NULL;
-    /* trace streams the chunks rotate over: with 2, chunk k + 2 cannot start before chunk k
-     * has drained (stream order), so two chunk tails can stall the pipeline; with up to 4
-     * every chunk is queued at once and the GPU takes their workgroups as CUs free up */
-    int nst = env_int("BHRT_BATCH_STREAMS", 4);
+    /* trace streams the chunks rotate over (BHRT_BATCH_STREAMS): 2 -- with 4, every chunk
+     * queued at once, C2 camera rays ran 158 instead of 172 Mrays/s (profiles/r04) */
+    int nst = env_int("BHRT_BATCH_STREAMS", 2);
     if (nst < 1) nst = 1;
     if (nst > 4) nst = 4;
     struct timespec tt[4];

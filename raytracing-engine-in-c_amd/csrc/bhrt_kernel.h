@@ -112,6 +112,7 @@ typedef struct {
                              permutation of [0, n)); NULL = ray id order */
     int skip_redo;        /* the redo launch may be left out where no ray can be evicted
                              (geodesic.hip launch_trace_pair); BHRT_SKIP_REDO=0: always launch */
+    int block_lanes;      /* lanes per workgroup of the hot trace launch (64, 128 or 256) */
 } bhrt_kparams;
 
 /* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and

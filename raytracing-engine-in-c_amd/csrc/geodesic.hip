@@ -1428,7 +1428,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     if (MULTIQ && lane == 0) {
         s_q[wv][0] = 0u;
         s_q[wv][1] = 0u;
-        s_q[wv][2] = (blockIdx.x * BHRT_TRACE_WAVES_PER_BLOCK + wv) & (nq - 1u);
+        s_q[wv][2] = (blockIdx.x * (blockDim.x >> 6) + wv) & (nq - 1u);
         s_q[wv][3] = 0u;
     }
     constexpr bool COLD = BHRT_COLD_KP;
@@ -1713,10 +1713,10 @@ int device_cus(int dev) {
     return cus;
 }
 
-// resident workgroups of 256 lanes of kernel fn on device dev (the persistent grid)
-int resident_blocks(const void* fn, int dev) {
+// resident workgroups of `lanes` lanes of kernel fn on device dev (the persistent grid)
+int resident_blocks(const void* fn, int dev, int lanes = 256) {
     int per_cu = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, lanes, 0);
     if (per_cu <= 0) per_cu = 1;
     return device_cus(dev) * per_cu;
 }
@@ -1731,10 +1731,10 @@ int grid_for(const void* fn, int n) {
 
 // smallest shift with 2^shift >= (waves * claim_div) / 2^queue_bits, at least 1 (a grid of
 // fewer waves than queues claims half a queue's remainder at a time); 0 = exact claims
-int claim_shift(int blocks, int claim_div, int queue_bits) {
+int claim_shift(int blocks, int claim_div, int queue_bits, int lanes = 256) {
     if (claim_div <= 0) return 0;
     const unsigned long long wq =
-        ((unsigned long long)blocks * (256 / 64) * (unsigned)claim_div) >> queue_bits;
+        ((unsigned long long)blocks * (unsigned)(lanes / 64) * (unsigned)claim_div) >> queue_bits;
     int shift = 1;
     while (shift < 31 && (1ull << shift) < wq) shift++;
     return shift;
@@ -1742,25 +1742,30 @@ int claim_shift(int blocks, int claim_div, int queue_bits) {
 
 template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool INL>
 void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
-    // resident workgroups of the two instantiations, per device
-    static std::atomic<int> grid_cap[kMaxDev], grid_huge[kMaxDev];
+    // resident workgroups of the two instantiations, per device (and per hot block size:
+    // kp.block_lanes, 64/128/256 lanes -- a workgroup's slot frees only once ALL its waves
+    // have drained, so small launches prefer one wave per workgroup)
+    static std::atomic<int> grid_cap[kMaxDev][3], grid_huge[kMaxDev];
     const int dev = current_device();
-    int cap = grid_cap[dev].load(std::memory_order_relaxed);
+    const int lanes = kp.block_lanes == 64 || kp.block_lanes == 128 ? kp.block_lanes : 256;
+    const int bi = lanes == 64 ? 0 : lanes == 128 ? 1 : 2;
+    int cap = grid_cap[dev][bi].load(std::memory_order_relaxed);
     int cap_huge = grid_huge[dev].load(std::memory_order_relaxed);
     if (cap == 0 || cap_huge == 0) {
         cap = resident_blocks(
-            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, false, INL>), dev);
+            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, false, INL>), dev,
+            lanes);
         cap_huge = resident_blocks(
             reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, true, INL>), dev);
-        grid_cap[dev].store(cap, std::memory_order_relaxed);
+        grid_cap[dev][bi].store(cap, std::memory_order_relaxed);
         grid_huge[dev].store(cap_huge, std::memory_order_relaxed);
     }
-    int blocks = (kp.n + 255) / 256;
+    int blocks = (kp.n + lanes - 1) / lanes;
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     bhrt_kparams k = kp;
-    k.claim_shift = claim_shift(blocks, kp.claim_div, kp.queue_bits);
-    k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, 256, 0, st>>>(k);
+    k.claim_shift = claim_shift(blocks, kp.claim_div, kp.queue_bits, lanes);
+    k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, lanes, 0, st>>>(k);
     // A camera launch on the zero-acceleration paths (C4, C5) evicts no ray: its loop has no
     // sincos that can raise the large-argument flag (rotation_trig), and the one refill-time
     // test, |state[5]| < rot_vmax, holds for every camera ray (|state[5]| = |v_r| is a dot
