@@ -17,6 +17,11 @@ if [ -z "$SKIP_TESTS" ]; then
     || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; }
   tail -1 $OUT/smoke.log
 fi
+if [ -n "$PRE_AB" ]; then  # block-size knob on the C4 plan shard and whole frame
+  echo "== ab C4 plan-8 shard 0" && CFG=C4 VARIANTS="$PRE_AB" ROUNDS=2 EXTRA="--no-host-path --plan-gpus 8 --shard 0" bash tools/ab.sh || exit 1
+  echo "== ab C4" && CFG=C4 VARIANTS="$PRE_AB" ROUNDS=2 EXTRA="--no-host-path" bash tools/ab.sh || exit 1
+  echo "== ab C2" && CFG=C2 VARIANTS="$PRE_AB" ROUNDS=2 EXTRA="--no-host-path" bash tools/ab.sh || exit 1
+fi
 echo "== default bench" && timeout -k 10 400 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err \
   || { echo "bench failed"; tail -20 $OUT/bench_default.err; exit 1; }
 cat $OUT/bench_default.json
