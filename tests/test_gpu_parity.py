@@ -378,7 +378,7 @@ def test_claim_order_does_not_change_results(bhrt_lib, monkeypatch, cname):
             bhrt_lib.set_claim_order(bad.data_ptr(), n)
         # a set order applies to device-API frames only: the chunks of a host-buffer frame of
         # the same ray count never take it
-        perm = orders[2]
+        perm = next(o for o in orders if torch.is_tensor(o))  # the random permutation
         bhrt_lib.set_claim_order(perm.data_ptr(), n)
         host = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
         outs.append(host)
