@@ -172,17 +172,6 @@ class FramePipeline:
         if mode == "samples" and world > 1 and not set(self.gather) <= set(RGB_FIELDS):
             raise ValueError("samples mode reduces the colour planes only")
         self.works = [None] * self.nslots
-        # GPU frames: rank 0's assembly (and, at N = 1 with several shards, the local copy
-        # that stands in for the gather) runs on a stream of its own, so the render stream
-        # holds only the frames' launches: the next frame's kernel starts as soon as the
-        # previous one on its stream ends, not behind an image copy (a C4 shard of the 8-GPU
-        # plan renders in ~0.15 ms; the copy took ~0.1 ms of it). Events order the buffer
-        # reuse: a slot's frame buffer is rewritten only after its copy / gather read it, and
-        # its receive buffer only after its assembly read it.
-        cuda = torch.device(device).type == "cuda"
-        self.side = torch.cuda.Stream(device) if cuda else None
-        self.ev_read = [None] * self.nslots    # the slot's frame buffer has been read
-        self.ev_asm = [None] * self.nslots     # the slot's assembly has read its receive buffer
         self.frames = 0
         self.last = None
         self.images = self.gathered = self.colour = None
@@ -216,9 +205,6 @@ class FramePipeline:
     def next_buffer(self):
         slot = self.frames % self.nslots
         self._complete(slot)
-        if self.ev_read[slot] is not None:  # the render may overwrite what the copy read
-            torch.cuda.current_stream().wait_event(self.ev_read[slot])
-            self.ev_read[slot] = None
         return self.bufs[slot]
 
     def submit(self):
@@ -238,23 +224,11 @@ class FramePipeline:
             recv = list(self.host_recv[slot].unbind(0)) if self.rank == 0 else None
             self.works[slot] = dist.gather(self.host_send[slot], recv, dst=0, async_op=True)
         elif self.world > 1:
-            if self.ev_asm[slot] is not None:  # (the gather writes what the assembly reads)
-                torch.cuda.current_stream().wait_event(self.ev_asm[slot])
-                self.ev_asm[slot] = None
             recv = list(self.gathered[slot].unbind(0)) if self.rank == 0 else None
             self.works[slot] = dist.gather(fb.buf[a:b], recv, dst=0, async_op=True)
         else:
             if self.gathered is not None:  # one shard of several: place it in the image
-                if self.side is not None:
-                    rendered = torch.cuda.Event()
-                    rendered.record()
-                    self.side.wait_event(rendered)
-                    with torch.cuda.stream(self.side):
-                        self.gathered[slot][0].copy_(fb.buf[a:b])
-                        self.ev_read[slot] = torch.cuda.Event()
-                        self.ev_read[slot].record()
-                else:
-                    self.gathered[slot][0].copy_(fb.buf[a:b])
+                self.gathered[slot][0].copy_(fb.buf[a:b])
             self.works[slot] = True
         self.frames += 1
 
@@ -268,20 +242,12 @@ class FramePipeline:
         if w is None:
             return
         if w is not True:
-            w.wait()  # (the render stream: its next frame reuses the buffer the gather read)
+            w.wait()
             if self.staged and self.rank == 0:
                 self.gathered[slot].copy_(self.host_recv[slot])
         self.works[slot] = None
         if self.rank == 0:
-            if self.side is not None and not self.staged and self.mode == "shards":
-                with torch.cuda.stream(self.side):
-                    if w is not True:
-                        w.wait()  # the assembly stream waits for the gather too
-                    self.last = self._assemble(slot)
-                    self.ev_asm[slot] = torch.cuda.Event()
-                    self.ev_asm[slot].record()
-            else:
-                self.last = self._assemble(slot)
+            self.last = self._assemble(slot)
 
     # Per-frame host work is a handful of tensor ops: every view the assembly needs is built
     # once per slot (a C4 shard of an 8-GPU plan renders in ~0.1 ms, so per-frame Python
