@@ -80,6 +80,14 @@ def _launch_ranks():
 if __name__ == "__main__":
     _launch_ranks()
 
+# Hardware queues per process (HIP runtime knob, read when HIP initialises; the box's default is
+# 4). Every HIP stream is bound to one queue, streams beyond the count share queues round robin,
+# and work on one queue runs in order: with the torch default stream, the two render streams and
+# RCCL's stream of an N-GPU run, a shared queue would put a frame's gather behind the next
+# frame's trace kernel. 8 gives each of them a queue of its own.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
 
 import numpy as np  # noqa: E402

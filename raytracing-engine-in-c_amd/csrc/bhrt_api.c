@@ -279,8 +279,7 @@ static devctx_t* ctx_get(int device) {
     devctx_t* c = (devctx_t*)calloc(1, sizeof *c);
     if (!c) return NULL;
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void**)&c->d_ctl,
+    if (hipMalloc((void**)&c->d_ctl,
                   (size_t)BHRT_RING * BHRT_SLOT_WORDS * sizeof(unsigned long long)) != hipSuccess) {
         set_err("cannot create HIP stream / control blocks on device %d", device);
         free(c);
@@ -297,12 +296,6 @@ static devctx_t* ctx_get(int device) {
             free(c);
             return NULL;
         }
-    if (hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
-        set_err("cannot create the copy stream on device %d", device);
-        free(c);
-        return NULL;
-    }
     for (int i = 0; i < BHRT_MAX_CHUNKS; i++)
         if (hipEventCreateWithFlags(&c->chunk_done[i], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->chunk_copied[i], hipEventDisableTiming) != hipSuccess) {
@@ -325,6 +318,31 @@ static devctx_t* ctx_get(int device) {
 }
 
 static int ensure(void** p, size_t* cap, size_t need, int pinned);
+
+/* libbhrt's own streams of a context (the default launch stream, the second trace stream and
+ * the copy stream of the host-buffer paths), created on first use with c's device current:
+ * a caller that only drives the device API on its own streams (bench.py) never creates them,
+ * so they take none of the process's hardware queues (GPU_MAX_HW_QUEUES; streams beyond it
+ * share a queue, and work on a shared queue runs in order) */
+static int ctx_streams(devctx_t* c) {
+    if (c->stream && c->stream2 && c->copy) return 0;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != c->device) {
+        if (hipSetDevice(c->device) != hipSuccess) {
+            set_err("hipSetDevice(%d) failed", c->device);
+            return -1;
+        }
+    }
+    if ((!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) ||
+        (!c->stream2 && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) ||
+        (!c->copy && hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess)) {
+        set_err("cannot create libbhrt's streams on device %d", c->device);
+        if (cur >= 0 && cur != c->device) (void)hipSetDevice(cur);
+        return -1;
+    }
+    if (cur >= 0 && cur != c->device && hipSetDevice(cur) != hipSuccess) return -1;
+    return 0;
+}
 
 /* launch scratch of `stream` on this context, at least `bytes` */
 static void* stream_scratch(devctx_t* c, hipStream_t stream, size_t bytes);
@@ -596,7 +614,10 @@ static void fill_camera(bhrt_kparams* kp, const bhrt_camera* cam, int W, int H) 
 /* one timed trace-kernel launch on `stream` (the context's own if NULL) */
 static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     if (kp->n <= 0) return 0;
-    if (!stream) stream = c->stream;
+    if (!stream) {
+        if (ctx_streams(c)) return -1;
+        stream = c->stream;
+    }
     /* the redo list follows the initial-state table (one extra field of the allocation) */
     kp->redo = (int*)(kp->init + (size_t)BHRT_INIT_FIELDS * (size_t)kp->n);
     if (c->npend == BHRT_RING && harvest(c) != 0) return -1;
@@ -727,6 +748,7 @@ static int render_frame_device(const BlackHoleParams* bh, const AccretionDiskPar
     devctx_t* c = ctx_get(dev);
     if (!c) return -1;
     if (colour_args_bad(out, (int)method, dk != NULL, bh->spin != 0.0)) return -1;
+    if (!stream && ctx_streams(c)) return -1;
     void* scratch = stream_scratch(c, stream ? (hipStream_t)stream : c->stream,
                                    (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) *
                                        (size_t)nrows * (size_t)W);
@@ -764,6 +786,7 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
     if (colour_args_bad(out, (int)method, dk != NULL, bh->spin != 0.0)) return -1;
     devctx_t* c = ctx_get(current_device());
     if (!c) return -1;
+    if (!stream && ctx_streams(c)) return -1;
     void* scratch = stream_scratch(c, stream ? (hipStream_t)stream : c->stream,
                                    (size_t)(BHRT_INIT_FIELDS + 1) * sizeof(double) * (size_t)n);
     if (!scratch) return -1;
@@ -937,6 +960,7 @@ static void readback_finish(const shard_job* j, const bhrt_frame_soa* host, cons
 static int readback(shard_job* j, const bhrt_frame_soa* host, int W, const bhrt_rows* rows) {
     devctx_t* c = j->c;
     HIP_TRY(hipSetDevice(c->device));
+    if (ctx_streams(c)) return -1;
     const size_t bytes = wanted_bytes(j, host);
     if (ensure(&c->h_stage, &c->cap_stage, bytes ? bytes : 64, 1)) return -1;
     if (readback_issue(j, host, (char*)c->h_stage, c->stream, NULL, NULL, NULL)) return -1;
@@ -1025,7 +1049,7 @@ int bhrt_render_frame_gather(const BlackHoleParams* bh, const AccretionDiskParam
     while (S > 1 && H < S * B) S--; /* every shard at least one row block */
     if (ndev > S) ndev = S;
     devctx_t* rc = ctx_get(root);
-    if (!rc) return -1;
+    if (!rc || (!stream && ctx_streams(rc))) return -1;
     hipStream_t rs = stream ? (hipStream_t)stream : rc->stream;
     if (S == 1)
         return render_frame_device(bh, dk, cfg, cam, W, H, NULL, method, flags, out, rs, 0);
@@ -1037,6 +1061,10 @@ int bhrt_render_frame_gather(const BlackHoleParams* bh, const AccretionDiskParam
         devctx_t* c = ctx_get(d);
         if (!c || hipSetDevice(d) != hipSuccess) {
             if (c) set_err("hipSetDevice(%d) failed", d);
+            rc_all = -1;
+            break;
+        }
+        if (k > 0 && ctx_streams(c)) {
             rc_all = -1;
             break;
         }
@@ -1138,11 +1166,11 @@ static void drain_devices(int ndev) {
     for (int d = 0; d < ndev; d++) {
         devctx_t* c = g_ctx[d];
         if (!c || hipSetDevice(d) != hipSuccess) continue;
-        (void)hipStreamSynchronize(c->stream);
-        (void)hipStreamSynchronize(c->stream2);
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        if (c->stream2) (void)hipStreamSynchronize(c->stream2);
         for (int i = 0; i < 2; i++)
             if (c->xs[i]) (void)hipStreamSynchronize(c->xs[i]);
-        (void)hipStreamSynchronize(c->copy);
+        if (c->copy) (void)hipStreamSynchronize(c->copy);
     }
     memcpy(g_err, err, sizeof err);
 }
@@ -1282,6 +1310,7 @@ static int frame_enqueue(host_frame* f, const BlackHoleParams* bh, const Accreti
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
         HIP_TRY(hipSetDevice(d));
+        if (ctx_streams(c)) return -1;
         size_t dev_bytes = 0;
         for (int k = 0; k < K; k++) {
             bhrt_rows* r = &f->rows[k][d];
@@ -1422,6 +1451,7 @@ int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
         HIP_TRY(hipSetDevice(d));
+        if (ctx_streams(c)) return -1;
         long m = base[d + 1] - base[d];
         jobs[d].c = c;
         jobs[d].n = m;
@@ -1541,6 +1571,7 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
         HIP_TRY(hipSetDevice(d));
+        if (ctx_streams(c)) return -1;
         for (int i = 0; i + 2 < nst; i++)
             if (!c->xs[i]) HIP_TRY(hipStreamCreateWithFlags(&c->xs[i], hipStreamNonBlocking));
         const long m = ms[d];
@@ -1672,7 +1703,7 @@ RayTraceResult integrate_photon_path(const Vector4D* position, const Vector3D* d
     if (!position || !direction || check_scene(bh, cfg)) return RAY_ERROR;
     int dev = current_device();
     devctx_t* c = ctx_get(dev);
-    if (!c) return RAY_ERROR;
+    if (!c || ctx_streams(c)) return RAY_ERROR;
     const int record = path != NULL && num_positions != NULL &&
                        (max_positions > 0 || *num_positions < max_positions);
     const int num_in = (path && max_positions <= 0 && num_positions) ? *num_positions : 0;
