@@ -4,9 +4,10 @@ One "step" = one camera frame of the workload traced by libbhrt.so with every in
 on the device: the frame kernel launch, plus (N > 1) the frame's single RCCL collective and
 its assembly on rank 0 (bhrt/dist_frame.py FramePipeline; the collective of frame i overlaps
 the rendering of frame i+1, and the timed region ends after the last one). Consecutive frames
-alternate between two HIP streams (--streams 2, the default), so the workgroups of frame i+1
-take the CUs that frame i's tail -- its last, longest rays draining -- leaves idle
-(tools/wave_tail.py: ~9% of a lone C2 launch); --streams 1 runs the frames back to back.
+alternate between HIP streams, so the workgroups of frame i+1 take the CUs that frame i's tail
+-- its last, longest rays draining -- leaves idle (tools/wave_tail.py: ~9% of a lone C2
+launch): two streams, or four for short frames (--streams auto, the default: a frame under
+0.4 ms, or too few rays to fill the chip's resident waves); --streams 1 runs them back to back.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--camera B]
 
@@ -104,6 +105,11 @@ FIELDS = abi.SOA_FIELDS
 # CPU-baseline row sample per config: ~1-3 s wall of the compiled reference on the GPU box's
 # 16 host cores (15-50 core-seconds)
 CPU_ROWS_STRIDE = {"C1": 1, "C2": 27, "C3": 27, "C4": 4, "C5": 3}
+# --streams auto: four frames in flight instead of two when a frame is short or small. Same-box
+# A/B (profiles/r04/session_f_streams/run2_warmed.txt): 4 streams C1 +6.5%, C3 +4.5%, the C4 8-GPU-plan
+# shard 0.186 -> 0.157 ms; C2 -1%, C4 full frame -1%, C5 -2%.
+AUTO_SHORT_MS = 0.4
+AUTO_FILL_RAYS = 256 * 4 * 4 * 64  # 4 waves per SIMD x 4 SIMDs x 256 CUs x 64 lanes
 
 
 def parse():
@@ -121,10 +127,12 @@ def parse():
     p.add_argument("--no-host-path", action="store_true",
                    help="skip the host-buffer leg (its chunked launches would mix into a "
                         "profiler's per-launch kernel averages)")
-    p.add_argument("--streams", type=int, default=2,
+    p.add_argument("--streams", default="auto",
                    help="consecutive frames alternate between this many HIP streams (1-4; "
                         "one frame buffer each), so the next frames' rays fill the CUs the tail "
-                        "of the current frame frees")
+                        "of the current frame frees; auto (default): 2, or 4 when calibration "
+                        "frames after the warm-up take under AUTO_SHORT_MS or the frame has "
+                        "fewer rays than AUTO_FILL_RAYS")
     p.add_argument("--weak-mode", choices=("tiles", "samples"), default="tiles",
                    help="weak configs at N GPUs: tiles = N shards of a frame (default); "
                         "samples = N sub-pixel sample planes of the configuration frame "
@@ -180,8 +188,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if not 1 <= args.streams <= 4:  # FramePipeline keeps one buffer slot per stream
-        raise SystemExit("--streams must be 1..4")
+    auto = args.streams == "auto"
+    if not auto and args.streams not in ("1", "2", "3", "4"):
+        raise SystemExit("--streams must be 1..4 or auto")
+    nstreams = 2 if auto else int(args.streams)  # FramePipeline keeps one buffer slot per stream
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # rehearsal of the N-GPU path on a one-GPU box: every rank on GPU 0, gloo collectives
@@ -240,9 +250,10 @@ def main():
     fields = FIELDS + DISPLAY_FIELD if args.gather == "rgba8" else FIELDS
     pipe = FramePipeline(n, device, world, rank, "samples" if samples else "shards", H, W, B,
                          fields, shards=S, gather=gather, first_shard=shard - rank,
-                         slots=args.streams)
-    streams = ([torch.cuda.current_stream()] if args.streams <= 1 else
-               [torch.cuda.Stream(device) for _ in range(args.streams)])
+                         slots=4 if auto else nstreams)
+    streams = ([torch.cuda.current_stream()] if nstreams <= 1 else
+               [torch.cuda.Stream(device) for _ in range(4 if auto else nstreams)])
+    active = [nstreams]
     frame_no = [0]
 
     def step():
@@ -251,7 +262,7 @@ def main():
         # the next frame's workgroups take those CUs (tools/wave_tail.py measures the tail).
         # A frame buffer slot is reused `streams` frames later (two with one stream), on the
         # same stream.
-        s = streams[frame_no[0] % len(streams)]
+        s = streams[frame_no[0] % active[0]]
         frame_no[0] += 1
         with torch.cuda.stream(s):
             fb = pipe.next_buffer()
@@ -262,10 +273,33 @@ def main():
     # every stream renders at least one untimed frame: a stream's first launch (its hardware
     # queue set up on first use, the slot's assembly views built) stays out of the timed region
     # even when --warmup is below --streams (then "warmup" reports the frames actually run)
-    warmup = max(args.warmup, len(streams))
+    warmup = max(args.warmup, nstreams)
     for _ in range(warmup):
         step()
     pipe.finish()
+    calib_ms = None
+    if auto:
+        # calibration: 4 frames on 2 streams (untimed); the ranks agree on the slowest
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        for _ in range(4):
+            step()
+        pipe.finish()
+        torch.cuda.synchronize()
+        calib_ms = (time.perf_counter() - tc) / 4 * 1e3
+        if world > 1:
+            t = torch.tensor([calib_ms], dtype=torch.float64,
+                             device="cpu" if shared else device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            calib_ms = t.item()
+        if calib_ms < AUTO_SHORT_MS or rays_frame // max(world, 1) < AUTO_FILL_RAYS:
+            # four streams; slot k of the pipeline stays on stream k from here on (frame_no
+            # and the pipeline's frame count advance together, and all work above is done)
+            active[0] = 4
+            for _ in range(4):  # each new stream's first launch, untimed
+                step()
+            pipe.finish()
+        warmup += 4 + (4 if active[0] == 4 else 0)
     torch.cuda.synchronize()
     lib.stats(reset=True)
     if world > 1:
@@ -305,7 +339,7 @@ def main():
     # next frame fills the CUs the current one's tail frees) and each launch's own start..end
     # interval double-counts the overlap, so the busy span of all timed launches / launches
     span_ms = st["span_ms"] / launches
-    dur_ms = span_ms if len(streams) > 1 else kern_ms
+    dur_ms = span_ms if active[0] > 1 else kern_ms
     f_launch = flops(st, c.method) / launches
     achieved = f_launch / (dur_ms * 1e-3) / 1e12
     prof = pmc_profile(args.config)
@@ -355,10 +389,14 @@ def main():
             "name": "k_trace (persistent, wave refill)",
             "avg_ms": round(dur_ms, 4),
             "duration": ("busy span of the timed launches (HIP events, first start to last "
-                         "end) / launches: frames alternate between 2 streams and overlap"
-                         if len(streams) > 1 else "per-launch HIP-event duration, averaged"),
+                         f"end) / launches: frames alternate between {active[0]} streams and "
+                         "overlap" if active[0] > 1 else "per-launch HIP-event duration, "
+                         "averaged"),
             "event_avg_ms": round(kern_ms, 4),
-            "streams": len(streams),
+            "streams": active[0],
+            "streams_policy": (f"auto: calibration frame {calib_ms:.3f} ms (4 streams under "
+                               f"{AUTO_SHORT_MS} ms or under {AUTO_FILL_RAYS} rays per GPU)"
+                               if auto else "fixed (--streams)"),
             "iterations_per_launch": st["iterations"] / max(st["launches"], 1),
             "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 4),
             "mean_iterations_per_ray": st["iterations"] / max(st["rays"], 1),
