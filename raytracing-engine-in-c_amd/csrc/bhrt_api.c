@@ -161,6 +161,7 @@ typedef struct {
     hipEvent_t g_done, g_copied, g_wait;
     int g_wait_pending;
     unsigned long long peer_on; /* bit d: peer access to device d enabled from this device */
+    void* h_zero; /* pinned zeros, one control region: its reset as a DMA copy (ctl_reset) */
 } devctx_t;
 
 static _Thread_local devctx_t* g_ctx[BHRT_MAX_DEV];
@@ -313,6 +314,12 @@ static devctx_t* ctx_get(int device) {
                     free(c);
                     return NULL;
                 }
+    if (hipHostMalloc(&c->h_zero, BHRT_SLOT_WORDS * sizeof(unsigned long long), 0) != hipSuccess) {
+        set_err("hipHostMalloc failed");
+        free(c);
+        return NULL;
+    }
+    memset(c->h_zero, 0, BHRT_SLOT_WORDS * sizeof(unsigned long long));
     g_ctx[device] = c;
     return c;
 }
@@ -552,6 +559,7 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
  * integrate_photon_path's origin-only set-up (raytracer.c:355-466, spacetime.c:15-33,
  * 201-237): every camera ray shares the origin, so its spherical coordinates, their sin/cos
  * and the metric there are computed once, here, with the same libm calls as the reference. */
+static void fill_origin(bhrt_kparams* kp, const Vector3D* origin);
 static void fill_camera(bhrt_kparams* kp, const bhrt_camera* cam, int W, int H) {
     bhrt_camera_k* k = &kp->cam;
     double aspect = (double)W / (double)H;
@@ -572,11 +580,18 @@ static void fill_camera(bhrt_kparams* kp, const bhrt_camera* cam, int W, int H) 
     k->height = H;
     k->inv_width = 1.0 / (double)W;
     k->inv_block = 1.0 / (double)k->rows.row_block;
-    k->pos[0] = cam->position.x;
-    k->pos[1] = cam->position.y;
-    k->pos[2] = cam->position.z;
+    fill_origin(kp, &cam->position);
+}
+
+/* integrate_photon_path's origin-only set-up for rays that share `origin` (a camera frame, or
+ * a ray array whose every origin is this one: shared_origin) */
+static void fill_origin(bhrt_kparams* kp, const Vector3D* origin) {
+    bhrt_camera_k* k = &kp->cam;
+    k->pos[0] = origin->x;
+    k->pos[1] = origin->y;
+    k->pos[2] = origin->z;
     Vector3D sph;
-    cartesian_to_spherical(&cam->position, &sph);
+    cartesian_to_spherical(origin, &sph);
     double r = sph.x, th = sph.y, ph = sph.z;
     double st = sin(th), ct = cos(th), sp = sin(ph), cp = cos(ph);
     k->r0 = r;
@@ -625,10 +640,15 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
     kp->ctl = c->d_ctl + (size_t)slot * BHRT_SLOT_WORDS;
     kp->qhead = kp->ctl + BHRT_QHEAD_OFF;
-    HIP_TRY(hipMemsetAsync(kp->ctl, 0,
-                           (BHRT_QHEAD_OFF + ((size_t)kp->queue_stride << kp->queue_bits)) *
-                               sizeof(unsigned long long),
-                           stream));
+    /* the control region is reset by a DMA copy of pinned zeros: a memset is a fill kernel,
+     * which waits for a free wave slot -- behind the persistent trace kernel of the previous
+     * launch on another stream -- before this launch can start (BHRT_CTL_COPY=0: memset) */
+    const size_t ctl_bytes =
+        (BHRT_QHEAD_OFF + ((size_t)kp->queue_stride << kp->queue_bits)) * sizeof(unsigned long long);
+    if (env_int("BHRT_CTL_COPY", 1))
+        HIP_TRY(hipMemcpyAsync(kp->ctl, c->h_zero, ctl_bytes, hipMemcpyHostToDevice, stream));
+    else
+        HIP_TRY(hipMemsetAsync(kp->ctl, 0, ctl_bytes, stream));
     if (!c->span_on) {
         HIP_TRY(hipEventRecord(c->span_ref, stream));
         c->span_on = 1;
@@ -775,10 +795,13 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
     return render_frame_device(bh, dk, cfg, cam, W, H, rows, method, flags, out, stream, 1);
 }
 
-int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
-                           const AccretionDiskParams* dk, const SimulationConfig* cfg,
-                           IntegrationMethod method, int flags, const bhrt_frame_soa* out,
-                           void* stream) {
+/* origin: non-NULL when the host knows every ray of d_rays starts at *origin (shared_origin):
+ * the origin's set-up is then done once here, as for a camera frame, and the trace kernel sets
+ * each ray up from its direction alone (no k_init table) */
+static int trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
+                             const AccretionDiskParams* dk, const SimulationConfig* cfg,
+                             IntegrationMethod method, int flags, const bhrt_frame_soa* out,
+                             void* stream, const Vector3D* origin) {
     if (check_scene(bh, cfg) || !d_rays || !out || n < 0) {
         if (!g_err[0]) set_err("invalid argument");
         return -1;
@@ -797,7 +820,29 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
     kp.init = (double*)scratch;
     kp.n = n;
     kp.out = *out;
+    if (origin && env_int("BHRT_SHARED_ORIGIN", 1)) {
+        fill_origin(&kp, origin);
+        kp.rays_shared = 1;
+    }
     return launch(c, &kp, (hipStream_t)stream);
+}
+
+int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
+                           const AccretionDiskParams* dk, const SimulationConfig* cfg,
+                           IntegrationMethod method, int flags, const bhrt_frame_soa* out,
+                           void* stream) {
+    return trace_rays_device(d_rays, n, bh, dk, cfg, method, flags, out, stream, NULL);
+}
+
+/* whether rays[0, n) all start at rays[0].origin (bit for bit) */
+static int shared_origin(const Ray* rays, long n, int nthreads) {
+    if (n <= 0) return 0;
+    const Vector3D o = rays[0].origin;
+    int diff = 0;
+#pragma omp parallel for schedule(static) reduction(| : diff) num_threads(nthreads) if (n >= 65536)
+    for (long i = 1; i < n; i++)
+        diff |= memcmp(&rays[i].origin, &o, sizeof o) != 0;
+    return !diff;
 }
 
 /* ---- host-buffer paths: device SoA block <-> caller SoA ---- */
@@ -1459,8 +1504,9 @@ int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
         if (device_soa(c, m, host, (int)method, dk != NULL, bh->spin != 0.0, &jobs[d].dev)) return -1;
         HIP_TRY(hipMemcpyAsync(c->d_rays, rays + base[d], (size_t)m * sizeof(Ray),
                                hipMemcpyHostToDevice, c->stream));
-        if (bhrt_trace_rays_device((const Ray*)c->d_rays, (int)m, bh, dk, cfg, method, flags,
-                                   &jobs[d].dev, c->stream))
+        const int shared = shared_origin(rays + base[d], m, host_threads());
+        if (trace_rays_device((const Ray*)c->d_rays, (int)m, bh, dk, cfg, method, flags,
+                              &jobs[d].dev, c->stream, shared ? &rays[base[d]].origin : NULL))
             return -1;
     }
     for (int d = 0; d < ndev; d++) {
@@ -1595,16 +1641,21 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                 Ray* hr = (Ray*)c->h_rays + a;
                 const Ray* src = rays + d0s[d];
                 const long nbk = (m + BHRT_BATCH_BLOCK - 1) / BHRT_BATCH_BLOCK;
-#pragma omp parallel for schedule(static) num_threads(stage_threads) if (nbk >= 4)
+                const Vector3D o = src[0].origin;
+                int diff = 0; /* does any ray of the chunk start elsewhere than src[0]? */
+#pragma omp parallel for schedule(static) reduction(| : diff) num_threads(stage_threads) if (nbk >= 4)
                 for (long j = 0; j < nbk; j++) { /* local block j = block k + j K of the device */
                     const long b0 = (k + j * K) * BHRT_BATCH_BLOCK;
                     const long len = md - b0 < BHRT_BATCH_BLOCK ? md - b0 : BHRT_BATCH_BLOCK;
-                    memcpy(hr + j * BHRT_BATCH_BLOCK, src + b0, (size_t)len * sizeof(Ray));
+                    Ray* dst = hr + j * BHRT_BATCH_BLOCK;
+                    memcpy(dst, src + b0, (size_t)len * sizeof(Ray));
+                    for (long i = 0; i < len; i++) /* (the block is in cache after the copy) */
+                        diff |= memcmp(&dst[i].origin, &o, sizeof o) != 0;
                 }
                 HIP_TRY(hipMemcpyAsync((Ray*)c->d_rays + a, hr, (size_t)m * sizeof(Ray),
                                        hipMemcpyHostToDevice, st));
-                if (bhrt_trace_rays_device((const Ray*)c->d_rays + a, (int)m, bh, dk, cfg,
-                                           INTEGRATOR_RK4, 0, &jobs[k][d].dev, st))
+                if (trace_rays_device((const Ray*)c->d_rays + a, (int)m, bh, dk, cfg,
+                                      INTEGRATOR_RK4, 0, &jobs[k][d].dev, st, diff ? NULL : &o))
                     return -1;
             }
             HIP_TRY(hipEventRecord(c->chunk_done[k], st));

@@ -57,7 +57,8 @@ typedef struct {
     int width, height;
     bhrt_rows rows;
     double inv_width, inv_block;     /* RN(1 / width), RN(1 / rows.row_block)  */
-    /* shared origin (integrate_photon_path set-up, raytracer.c:355-466) */
+    /* shared origin (integrate_photon_path set-up, raytracer.c:355-466); also filled for ray
+     * arrays with one origin (bhrt_kparams.rays_shared) */
     double pos[3];                   /* Cartesian origin                        */
     double r0, th0, ph0;             /* cartesian_to_spherical(origin)          */
     double st_cp, st_sp, ct, ct_cp, ct_sp, st, neg_sp, cp, r_st; /* trig products */
@@ -113,6 +114,9 @@ typedef struct {
     int skip_redo;        /* the redo launch may be left out where no ray can be evicted
                              (geodesic.hip launch_trace_pair); BHRT_SKIP_REDO=0: always launch */
     int block_lanes;      /* lanes per workgroup of the hot trace launch (64, 128 or 256) */
+    int rays_shared;      /* BHRT_SRC_RAYS whose every origin is cam.pos (the host checked):
+                             cam's origin block is filled as for a camera frame, and the
+                             trace kernel sets rays up from their directions (no k_init) */
 } bhrt_kparams;
 
 /* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and

@@ -811,6 +811,31 @@ __device__ __forceinline__ void ray_init_camera(Ray_& R, const bhrt_camera_k& cm
     R.k = 0;
 }
 
+// A ray of an array whose rays all start at the launch's shared origin (kp.rays_shared): the
+// origin part of the set-up is the host's (cm, as for a camera frame); the direction is the
+// array's, kept as given for the disk test (Ray.direction) and normalised for the velocities,
+// as ray_init_general does.
+__device__ __forceinline__ void ray_init_shared(Ray_& R, const bhrt_camera_k& cm, const Ray* rays,
+                                                int i) {
+    R.dx = rays[i].direction.x;
+    R.dy = rays[i].direction.y;
+    R.dz = rays[i].direction.z;
+    double nx, ny, nz;
+    normalize3(R.dx, R.dy, R.dz, nx, ny, nz);
+    init_velocity(R, nx, ny, nz, cm.r0, cm.st_cp, cm.st_sp, cm.ct, cm.ct_cp, cm.ct_sp, cm.st,
+                  cm.neg_sp, cm.cp, cm.r_st, cm.st_tiny != 0, cm.g_tt, cm.g_rr, cm.g_hh,
+                  cm.use_approx != 0);
+    R.y[0] = 0.0;
+    R.y[1] = cm.r0;
+    R.y[2] = cm.th0;
+    R.y[3] = cm.ph0;
+    R.px = cm.p0[0];
+    R.py = cm.p0[1];
+    R.pz = cm.p0[2];
+    R.dist = 0.0;
+    R.k = 0;
+}
+
 // check_disk_intersection (raytracer.c:159-196), plane "normal" = previous path point n,
 // straight-line: every lane forms t, the candidate point and the radial test, and the four
 // rejections are ONE mask (a per-test early return became nested exec-mask regions, ~50 SALU
@@ -1383,11 +1408,14 @@ constexpr int unroll_n() {
 // HUGE = false: the hot instantiation, rays [0, kp.n) from the queues kp.qhead. A ray that
 // needs a large-argument sincos (bhrt_sincos) is dropped and its id appended to kp.redo
 // (count ctl[6]). HUGE = true: re-traces kp.redo[0, ctl[6]) from queue head ctl[7].
-// INL: camera launch whose rays are set up here, at refill (ray_init_camera), instead of
-// being loaded from k_init's 168-byte table: used where rays are short-lived (Kerr, RKF45), so
-// refills are frequent and each table load stalls its wave on HBM latency.
+// INL: rays set up here, at refill, instead of being loaded from k_init's table: 1 = camera
+// launch (ray_init_camera), 2 = ray array with one shared origin (ray_init_shared: the origin's
+// set-up from the host, the direction from the array). Used where rays are short-lived (Kerr,
+// RKF45), so refills are frequent and each table load stalls its wave on HBM latency, and on the
+// a = 0 RK4 disk path; ray arrays from trace_rays_batch take 2, so a chunk's
+// trace depends on its upload alone (no set-up kernel queued behind the previous chunk's).
 // The sin/cos anchors of the shared origin are the same for every ray: computed once per wave.
-template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, bool INL = false>
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, int INL = 0>
 __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const unsigned long long total =
         HUGE ? *(volatile unsigned long long*)(kp.ctl + 6) : (unsigned long long)kp.n;
@@ -1517,7 +1545,10 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     rid = HUGE ? kp.redo[id] : (kp.src == BHRT_SRC_CAMERA ? claim_ray(kc, qpos) : qpos);
                     // (the redo list holds ray ids; the k_init table is in claim order)
                     if (INL || (HUGE && (kp.order || kp.cam.tiles_per_row))) {
-                        ray_init_camera(R, kc.cam, rid);
+                        if constexpr (INL == 2)
+                            ray_init_shared(R, kc.cam, kc.rays, rid);
+                        else
+                            ray_init_camera(R, kc.cam, rid);
                         R.s1 = as1;
                         R.c1 = ac1;
                         R.s2 = as2;
@@ -1740,7 +1771,7 @@ int claim_shift(int blocks, int claim_div, int queue_bits, int lanes = 256) {
     return shift;
 }
 
-template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool INL>
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, int INL>
 void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     // resident workgroups of the two instantiations, per device (and per hot block size:
     // kp.block_lanes, 64/128/256 lanes -- a workgroup's slot frees only once ALL its waves
@@ -1794,8 +1825,13 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
     // 168-byte table -- 0.7 GB written and read per 8K shard -- outweighs the set-up: +1.5%
     // same-box, profiles/r02_ab_v20_occupancy.txt; it lost 5% on round 1's 193-attempt slab,
     // r01_ab_v10.txt).
+    // Ray arrays with one shared origin (kp.rays_shared) the same way where a camera frame
+    // would (mode 2: the direction from the array).
     constexpr bool CAN_INL = DISK ? true : (METHOD == INTEGRATOR_RKF45 && !SPIN0);
-    const bool inl = CAN_INL && kp.src == BHRT_SRC_CAMERA && fabs(kp.cam.r0) < 1048576.0;
+    const int inl = !CAN_INL || !(fabs(kp.cam.r0) < 1048576.0) ? 0
+                  : kp.src == BHRT_SRC_CAMERA                  ? 1
+                  : kp.rays_shared                             ? 2
+                                                               : 0;
     if (inl)
         ;
     else if (kp.src == BHRT_SRC_CAMERA)
@@ -1806,12 +1842,14 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
                                          kp.n), 256, 0, st>>>(kp);
     if (ev0) (void)hipEventRecord(ev0, st);
     if constexpr (CAN_INL) {
-        if (inl)
-            launch_trace_pair<METHOD, DISK, SPIN0, FAR, true>(kp, st);
+        if (inl == 1)
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, 1>(kp, st);
+        else if (inl == 2)
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, 2>(kp, st);
         else
-            launch_trace_pair<METHOD, DISK, SPIN0, FAR, false>(kp, st);
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, 0>(kp, st);
     } else {
-        launch_trace_pair<METHOD, DISK, SPIN0, FAR, false>(kp, st);
+        launch_trace_pair<METHOD, DISK, SPIN0, FAR, 0>(kp, st);
     }
     if (ev1) (void)hipEventRecord(ev1, st);
     if (!kp.colour_fused && (kp.out.rgb_r || kp.out.rgba32f || kp.out.rgba8)) {
@@ -1827,7 +1865,9 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
 
 template <int METHOD, bool DISK, bool SPIN0>
 int dispatch_far(const bhrt_kparams& kp, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-    const bool far = kp.src != BHRT_SRC_CAMERA || kp.cam.use_approx;
+    // a camera frame, or a ray array with one shared origin, knows from the host whether its
+    // origin is beyond 15 rs (use_analytic_approx); other ray arrays assume some ray may be
+    const bool far = (kp.src == BHRT_SRC_CAMERA || kp.rays_shared) ? kp.cam.use_approx != 0 : true;
     return far ? launch_t<METHOD, DISK, SPIN0, true>(kp, st, e0, e1)
                : launch_t<METHOD, DISK, SPIN0, false>(kp, st, e0, e1);
 }

@@ -817,6 +817,36 @@ def test_large_batch_pipelined_equals_soa_trace(bhrt_lib, n):
     assert not hits["sky_direction"][~esc].any()
 
 
+@pytest.mark.parametrize("cname", ["C1", "C2", "C3", "C4", "C5"])
+def test_shared_origin_ray_arrays_vs_oracle(bhrt_lib, oracle, monkeypatch, cname):
+    """Ray arrays whose rays all start at one point (a camera's rays passed as Ray[]: the
+    visualizer's trace_rays_batch) are set up inside the trace kernel from the host's origin
+    block, as camera frames are (kparams.rays_shared; C1 keeps the set-up pass, with the
+    far-field decision from the host): every ray against the oracle, through the one-launch
+    path and the pipelined trace_rays_batch, which must agree bit for bit; with
+    BHRT_SHARED_ORIGIN=0 (the per-ray k_init table) the same rays agree with the oracle too."""
+    c = configs.CONFIGS[cname]
+    bh, dk, cfg = c.scene()
+    W, H = 96, 64
+    rays = configs.camera_rays(configs.camera("B"), W, H)
+    want = oracle.trace_rays(rays, bh, dk, cfg, c.method, c.flags)
+    got = bhrt_lib.trace_rays(rays, bh, dk, cfg, c.method, c.flags)
+    compare(got, want, RTOL, sky_pinned(c.method), f"{cname} shared origin")
+    if c.method == abi.INTEGRATOR_RK4:  # trace_rays_batch is RK4 (trace_ray's integrator)
+        big = np.resize(rays, 1 << 16)  # >= 65536 rays: the pipelined chunks
+        ref = bhrt_lib.trace_rays(big, bh, dk, cfg)
+        rc, hits = bhrt_lib.trace_rays_batch(big, bh, dk, cfg)
+        assert rc == 0
+        assert np.array_equal(hits["result"], ref["result"])
+        assert np.array_equal(hits["steps"], ref["steps"])
+        for i, ax in enumerate("xyz"):
+            assert np.array_equal(hits["hit_position"][:, i], ref["hit_" + ax], equal_nan=True)
+        assert np.array_equal(hits["distance"], ref["distance"], equal_nan=True)
+    monkeypatch.setenv("BHRT_SHARED_ORIGIN", "0")
+    gen = bhrt_lib.trace_rays(rays, bh, dk, cfg, c.method, c.flags)
+    compare(gen, want, RTOL, sky_pinned(c.method), f"{cname} per-ray set-up")
+
+
 def test_rkf45_accept_band(bhrt_lib):
     """The trace kernel's RKF45 accept test (geodesic.hip rkf45_accept): the
     division-free fast form -- q = err * rcp(scale) decides outside a +-2^-40 band around

@@ -5,8 +5,8 @@
       python3 tools/batch_probe.py
   python tools/batch_timeline.py D/.../run_kernel_trace.csv D/.../run_memory_copy_trace.csv
 
-Prints every kernel dispatch and copy of the LAST call (the events after the last idle gap
-longer than --gap ms that precedes the final --kernels trace dispatches), in start order and
+Prints every kernel dispatch and copy of one call (events are split into calls at idle gaps
+longer than --gap ms; --call picks among those with trace kernels, default the last), in start order and
 relative to the call's first event, then the union of busy time per kind: where the call's
 wall time goes besides tracing (the first upload before any kernel, the last chunk's
 download after the last kernel, gaps between them).
@@ -38,6 +38,7 @@ def main():
     ap.add_argument("kernels")
     ap.add_argument("copies")
     ap.add_argument("--gap", type=float, default=0.5, help="idle gap (ms) that separates calls")
+    ap.add_argument("--call", type=int, default=-1, help="which call with trace kernels (-1: last)")
     a = ap.parse_args()
     ev = []
     with open(a.kernels) as f:
@@ -59,7 +60,8 @@ def main():
         cur.append(e)
         end = e[1] if end is None else max(end, e[1])
     calls.append(cur)
-    last = calls[-1]
+    calls = [c for c in calls if any(n.startswith("k_trace") for _, _, _, n in c)]
+    last = calls[a.call]
     t0 = last[0][0]
     for s, e, k, n in last:
         print(f"{(s - t0) / 1e6:8.3f} .. {(e - t0) / 1e6:8.3f} ms  {(e - s) / 1e6:7.3f}  {k} {n}")

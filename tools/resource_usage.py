@@ -20,7 +20,7 @@ for l in out.splitlines():
     if m and cur:
         rows[cur][m.group(1).strip()] = m.group(2)
 for k, v in rows.items():
-    m = re.search(r"k_traceILi(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)E", k)
+    m = re.search(r"k_traceILi(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)EL[bi](\d)E", k)
     if not m:
         continue
     print("k_trace<%s>" % ",".join(m.groups()), "VGPR", v.get("VGPRs"), "SGPR", v.get("TotalSGPRs"),
