@@ -161,7 +161,6 @@ typedef struct {
     hipEvent_t g_done, g_copied, g_wait;
     int g_wait_pending;
     unsigned long long peer_on; /* bit d: peer access to device d enabled from this device */
-    void* h_zero; /* pinned zeros, one control region: its reset as a DMA copy (ctl_reset) */
 } devctx_t;
 
 static _Thread_local devctx_t* g_ctx[BHRT_MAX_DEV];
@@ -314,12 +313,6 @@ static devctx_t* ctx_get(int device) {
                     free(c);
                     return NULL;
                 }
-    if (hipHostMalloc(&c->h_zero, BHRT_SLOT_WORDS * sizeof(unsigned long long), 0) != hipSuccess) {
-        set_err("hipHostMalloc failed");
-        free(c);
-        return NULL;
-    }
-    memset(c->h_zero, 0, BHRT_SLOT_WORDS * sizeof(unsigned long long));
     g_ctx[device] = c;
     return c;
 }
@@ -640,15 +633,12 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
     kp->ctl = c->d_ctl + (size_t)slot * BHRT_SLOT_WORDS;
     kp->qhead = kp->ctl + BHRT_QHEAD_OFF;
-    /* the control region is reset by a DMA copy of pinned zeros: a memset is a fill kernel,
-     * which waits for a free wave slot -- behind the persistent trace kernel of the previous
-     * launch on another stream -- before this launch can start (BHRT_CTL_COPY=0: memset) */
-    const size_t ctl_bytes =
-        (BHRT_QHEAD_OFF + ((size_t)kp->queue_stride << kp->queue_bits)) * sizeof(unsigned long long);
-    if (env_int("BHRT_CTL_COPY", 1))
-        HIP_TRY(hipMemcpyAsync(kp->ctl, c->h_zero, ctl_bytes, hipMemcpyHostToDevice, stream));
-    else
-        HIP_TRY(hipMemsetAsync(kp->ctl, 0, ctl_bytes, stream));
+    /* (a fill kernel; a copy of pinned zeros measured the same -- small copies are blit
+     * kernels too -- profiles/r04/session_h_batch) */
+    HIP_TRY(hipMemsetAsync(kp->ctl, 0,
+                           (BHRT_QHEAD_OFF + ((size_t)kp->queue_stride << kp->queue_bits)) *
+                               sizeof(unsigned long long),
+                           stream));
     if (!c->span_on) {
         HIP_TRY(hipEventRecord(c->span_ref, stream));
         c->span_on = 1;
@@ -1565,23 +1555,94 @@ static void hit_fields(char* p, long n, bhrt_frame_soa* s) {
 #define HIT_BYTES (2 * sizeof(int32_t) + 8 * sizeof(double))
 
 /* Large batches: K chunks per device on alternating trace streams. A device's rays are cut into
- * blocks of BHRT_BATCH_BLOCK dealt round robin over the chunks (chunk k holds blocks k, k + K,
- * ...), so every chunk carries the same mix of short and long rays whatever the order of the
- * caller's array (row-major camera rays put the expensive rows in one contiguous quarter).
+ * blocks of BHRT_BATCH_BLOCK dealt over the chunks by a repeating pattern (chunk_plan: with
+ * equal weights block b goes to chunk b mod K), so every chunk carries the same mix of short
+ * and long rays whatever the order of the caller's array (row-major camera rays put the
+ * expensive rows in one contiguous quarter).
  * Launching chunk k first copies its blocks into consecutive pinned staging (OpenMP threads;
  * so the upload is asynchronous and overlaps the chunks already tracing); each chunk's results
  * come back in one copy on the copy stream, and the host packs a chunk into hits[] as soon as
  * it lands, with nthreads threads. BHRT_HOST_TIMING=1 prints where a call's time went. */
 #define BHRT_BATCH_BLOCK 1024L
 
-/* rays of chunk k when a device's m rays are dealt in blocks round robin over K chunks (only the
- * device's last block can be partial) */
-static long batch_chunk_rays(long m, int K, int k) {
+/* How a device's blocks are dealt over the K chunks: block b goes to chunk pat[b mod L], where
+ * chunk k holds w[k] of the L = sum(w) pattern positions, spread evenly over the pattern (each
+ * position goes to the chunk furthest behind its share), so a chunk of any weight samples the
+ * whole array. Weights let the first chunk be small (the GPU starts after a short upload) and
+ * the last one too (a short download and pack after the last trace); BHRT_BATCH_WEIGHTS
+ * ("1,5,5,4,1") overrides the equal default. */
+#define BHRT_PATTERN_MAX 64
+typedef struct {
+    int K, L;
+    int pat[BHRT_PATTERN_MAX];
+    int cnt[BHRT_MAX_CHUNKS];                   /* pattern positions of chunk k */
+    int pos[BHRT_MAX_CHUNKS][BHRT_PATTERN_MAX]; /* ... in increasing order */
+} chunk_plan;
+
+static void plan_chunks(chunk_plan* P, int K, const int* w) {
+    P->K = K;
+    P->L = 0;
+    for (int k = 0; k < K; k++) {
+        P->L += w[k];
+        P->cnt[k] = 0;
+    }
+    for (int p = 0; p < P->L; p++) {
+        int best = 0;
+        double lag = -1e300;
+        for (int k = 0; k < K; k++) { /* share due by position p + 1 minus what k has */
+            const double d = (double)w[k] * (p + 1) / P->L - P->cnt[k];
+            if (d > lag + 1e-12) {
+                lag = d;
+                best = k;
+            }
+        }
+        P->pat[p] = best;
+        P->pos[best][P->cnt[best]++] = p;
+    }
+}
+
+/* device block of chunk k's j-th block */
+static inline long plan_block(const chunk_plan* P, int k, long j) {
+    return (j / P->cnt[k]) * P->L + P->pos[k][j % P->cnt[k]];
+}
+
+/* rays of chunk k when a device's m rays are dealt by P (only the device's last block can be
+ * partial) */
+static long plan_rays(const chunk_plan* P, long m, int k) {
     const long nb = (m + BHRT_BATCH_BLOCK - 1) / BHRT_BATCH_BLOCK;
-    if (k >= nb) return 0;
-    long cnt = ((nb - 1 - k) / K + 1) * BHRT_BATCH_BLOCK;
-    if ((nb - 1) % K == k) cnt -= nb * BHRT_BATCH_BLOCK - m;
-    return cnt;
+    if (nb == 0 || P->cnt[k] == 0) return 0;
+    long blocks = (nb / P->L) * P->cnt[k];
+    for (int t = 0; t < P->cnt[k]; t++)
+        if (P->pos[k][t] < nb % P->L) blocks++;
+    long rays = blocks * BHRT_BATCH_BLOCK;
+    if (P->pat[(nb - 1) % P->L] == k) rays -= nb * BHRT_BATCH_BLOCK - m;
+    return rays;
+}
+
+/* the chunk plan of a batch call: BHRT_BATCH_WEIGHTS, else K equal chunks */
+static void batch_plan(chunk_plan* P, int K) {
+    int w[BHRT_MAX_CHUNKS], nw = 0, sum = 0;
+    const char* e = getenv("BHRT_BATCH_WEIGHTS");
+    while (e && *e && nw < BHRT_MAX_CHUNKS) {
+        char* end;
+        const long v = strtol(e, &end, 10);
+        if (end == e || v < 1 || v > BHRT_PATTERN_MAX) {
+            nw = 0;
+            break;
+        }
+        w[nw++] = (int)v;
+        sum += (int)v;
+        e = *end == ',' ? end + 1 : end;
+        if (*end != ',' && *end) {
+            nw = 0;
+            break;
+        }
+    }
+    if (nw < 1 || sum > BHRT_PATTERN_MAX || (e && *e)) {
+        nw = K;
+        for (int k = 0; k < K; k++) w[k] = 1;
+    }
+    plan_chunks(P, nw, w);
 }
 
 static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* bh,
@@ -1604,6 +1665,9 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
     int nst = env_int("BHRT_BATCH_STREAMS", 2);
     if (nst < 1) nst = 1;
     if (nst > 4) nst = 4;
+    chunk_plan P;
+    batch_plan(&P, K);
+    K = P.K;
     struct timespec tt[4];
     clock_gettime(CLOCK_MONOTONIC, &tt[0]);
     long d0s[BHRT_MAX_DEV], ms[BHRT_MAX_DEV];
@@ -1613,7 +1677,7 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
         d0s[d] = (long)n * d / ndev;
         ms[d] = (long)n * (d + 1) / ndev - d0s[d];
         off[0][d] = 0;
-        for (int k = 0; k < K; k++) off[k + 1][d] = off[k][d] + batch_chunk_rays(ms[d], K, k);
+        for (int k = 0; k < K; k++) off[k + 1][d] = off[k][d] + plan_rays(&P, ms[d], k);
         devctx_t* c = ctx_get(d);
         if (!c) return -1;
         HIP_TRY(hipSetDevice(d));
@@ -1644,8 +1708,8 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                 const Vector3D o = src[0].origin;
                 int diff = 0; /* does any ray of the chunk start elsewhere than src[0]? */
 #pragma omp parallel for schedule(static) reduction(| : diff) num_threads(stage_threads) if (nbk >= 4)
-                for (long j = 0; j < nbk; j++) { /* local block j = block k + j K of the device */
-                    const long b0 = (k + j * K) * BHRT_BATCH_BLOCK;
+                for (long j = 0; j < nbk; j++) { /* local block j = device block plan_block() */
+                    const long b0 = plan_block(&P, k, j) * BHRT_BATCH_BLOCK;
                     const long len = md - b0 < BHRT_BATCH_BLOCK ? md - b0 : BHRT_BATCH_BLOCK;
                     Ray* dst = hr + j * BHRT_BATCH_BLOCK;
                     memcpy(dst, src + b0, (size_t)len * sizeof(Ray));
@@ -1679,10 +1743,13 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
             hit_fields((char*)c->h_stage + (size_t)a * HIT_BYTES, m, &s);
             clock_gettime(CLOCK_MONOTONIC, &tt[3]);
             RayTraceHit* h = hits + d0s[d];
+            const long nbk = (m + BHRT_BATCH_BLOCK - 1) / BHRT_BATCH_BLOCK;
 #pragma omp parallel for schedule(static) num_threads(nthreads) if (m >= 65536)
-            for (long i = 0; i < m; i++) { /* local ray i: block k + (i / B) K of the device */
-                const long j = i / BHRT_BATCH_BLOCK;
-                pack_one(&h[(k + j * K) * BHRT_BATCH_BLOCK + (i - j * BHRT_BATCH_BLOCK)], &s, i);
+            for (long j = 0; j < nbk; j++) { /* local block j: rays [j B, j B + len) */
+                RayTraceHit* hb = h + plan_block(&P, k, j) * BHRT_BATCH_BLOCK;
+                const long i0 = j * BHRT_BATCH_BLOCK;
+                const long len = m - i0 < BHRT_BATCH_BLOCK ? m - i0 : BHRT_BATCH_BLOCK;
+                for (long t = 0; t < len; t++) pack_one(&hb[t], &s, i0 + t);
             }
             if (timing) {
                 struct timespec t4;

@@ -50,6 +50,7 @@ static void on_device(const void* p, size_t n, const char* what) {
 /* the value every field gets for image pixel / input ray v */
 static double enc(int f, long v) { return (double)v * 4.0 + f + 0.25; }
 
+static long g_shared_launches; /* ray launches that took the shared-origin set-up */
 int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0, void* ev1) {
     (void)stream; (void)ev0; (void)ev1;
     const long n = kp->n;
@@ -69,6 +70,14 @@ int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0, void* ev1
                 py = ((j / B) * kp->cam.rows.num_shards + kp->cam.rows.shard) * B + j % B;
             }
             v = py * W + px;
+        } else if (kp->rays_shared) { /* one origin (the host said so): the id rides in dx */
+            if (memcmp(&kp->rays[i].origin.x, &kp->cam.pos[0], 8) ||
+                memcmp(&kp->rays[i].origin.y, &kp->cam.pos[1], 8) ||
+                memcmp(&kp->rays[i].origin.z, &kp->cam.pos[2], 8)) {
+                fprintf(stderr, "rays_shared launch with a ray off the shared origin\n");
+                abort();
+            }
+            v = (long)kp->rays[i].direction.x;
         } else {
             v = (long)kp->rays[i].origin.x;
         }
@@ -85,6 +94,8 @@ int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0, void* ev1
             for (int c = 0; c < 4; c++) kp->out.rgba8[4 * i + c] = (uint8_t)(v + c);
     }
     kp->ctl[1] += (unsigned long long)n; /* rays */
+    if (kp->src == BHRT_SRC_RAYS && kp->rays_shared)
+        __atomic_fetch_add(&g_shared_launches, 1, __ATOMIC_RELAXED);
     return 0;
 }
 int bhrt_launch_path(const bhrt_kparams* kp, const double* o, const double* d, Vector3D* p,
@@ -239,13 +250,22 @@ static void run(BlackHoleParams* bh, SimulationConfig* cfg, AccretionDiskParams*
         CHECK(hipSetDevice(0) == hipSuccess, "reset device");
     }
     /* ray batches: SoA split over the devices, and the pipelined RayTraceHit path */
-    for (int pass = 0; pass < 2; pass++) {
+    /* pass 2: every ray at one origin (its id in direction.x): the shared-origin set-up */
+    for (int pass = 0; pass < 3; pass++) {
         const long n = pass ? 300001 : 100003;
         Ray* rays = (Ray*)calloc(n, sizeof(Ray));
         for (long i = 0; i < n; i++) {
-            rays[i].origin.x = (double)i;
+            if (pass == 2) {
+                rays[i].origin.x = 1.0;
+                rays[i].origin.y = -2.0;
+                rays[i].origin.z = 30.0;
+                rays[i].direction.x = (double)i;
+            } else {
+                rays[i].origin.x = (double)i;
+            }
             rays[i].direction.z = 1.0;
         }
+        const long shared0 = __atomic_load_n(&g_shared_launches, __ATOMIC_RELAXED);
         if (!pass) {
             host_soa h = soa_new(n, ALL, 0);
             CHECK(bhrt_trace_rays(rays, (int)n, bh, dk, cfg, INTEGRATOR_RK4, 0, &h.soa) == 0,
@@ -270,6 +290,10 @@ static void run(BlackHoleParams* bh, SimulationConfig* cfg, AccretionDiskParams*
                     bad++;
             }
             CHECK(bad == 0, "trace_rays_batch: %ld hits wrong", bad);
+            /* (the other thread's launches count too: only "at least one" is per-thread) */
+            if (pass == 2)
+                CHECK(__atomic_load_n(&g_shared_launches, __ATOMIC_RELAXED) > shared0,
+                      "shared-origin batch took the per-ray set-up");
             free(hits);
         }
         free(rays);
