@@ -785,14 +785,16 @@ int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParam
     return render_frame_device(bh, dk, cfg, cam, W, H, rows, method, flags, out, stream, 1);
 }
 
-/* origin: non-NULL when the host knows every ray of d_rays starts at *origin (shared_origin):
- * the origin's set-up is then done once here, as for a camera frame, and the trace kernel sets
- * each ray up from its direction alone (no k_init table) */
-static int trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
-                             const AccretionDiskParams* dk, const SimulationConfig* cfg,
-                             IntegrationMethod method, int flags, const bhrt_frame_soa* out,
-                             void* stream, const Vector3D* origin) {
-    if (check_scene(bh, cfg) || !d_rays || !out || n < 0) {
+/* origin: non-NULL when the host knows every ray starts at *origin (shared_origin): the
+ * origin's set-up is then done once here, as for a camera frame, and the trace kernel sets each
+ * ray up from its direction alone (no k_init table). The rays are d_rays (AoS), or -- with an
+ * origin only -- d_rays NULL and d_dirs their packed directions (3 doubles per ray: half the
+ * upload of trace_rays_batch's chunks). */
+static int trace_rays_device(const Ray* d_rays, const double* d_dirs, int n,
+                             const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                             const SimulationConfig* cfg, IntegrationMethod method, int flags,
+                             const bhrt_frame_soa* out, void* stream, const Vector3D* origin) {
+    if (check_scene(bh, cfg) || !(d_rays || (d_dirs && origin)) || !out || n < 0) {
         if (!g_err[0]) set_err("invalid argument");
         return -1;
     }
@@ -810,9 +812,11 @@ static int trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh
     kp.init = (double*)scratch;
     kp.n = n;
     kp.out = *out;
-    if (origin && env_int("BHRT_SHARED_ORIGIN", 1)) {
+    if (origin && (env_int("BHRT_SHARED_ORIGIN", 1) || !d_rays)) {
         fill_origin(&kp, origin);
         kp.rays_shared = 1;
+        kp.dirs = d_rays ? &d_rays[0].direction.x : d_dirs;
+        kp.dir_stride = d_rays ? (int)(sizeof(Ray) / sizeof(double)) : 3;
     }
     return launch(c, &kp, (hipStream_t)stream);
 }
@@ -821,7 +825,7 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
                            const AccretionDiskParams* dk, const SimulationConfig* cfg,
                            IntegrationMethod method, int flags, const bhrt_frame_soa* out,
                            void* stream) {
-    return trace_rays_device(d_rays, n, bh, dk, cfg, method, flags, out, stream, NULL);
+    return trace_rays_device(d_rays, NULL, n, bh, dk, cfg, method, flags, out, stream, NULL);
 }
 
 /* whether rays[0, n) all start at rays[0].origin (bit for bit) */
@@ -1495,7 +1499,7 @@ int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* bh,
         HIP_TRY(hipMemcpyAsync(c->d_rays, rays + base[d], (size_t)m * sizeof(Ray),
                                hipMemcpyHostToDevice, c->stream));
         const int shared = shared_origin(rays + base[d], m, host_threads());
-        if (trace_rays_device((const Ray*)c->d_rays, (int)m, bh, dk, cfg, method, flags,
+        if (trace_rays_device((const Ray*)c->d_rays, NULL, (int)m, bh, dk, cfg, method, flags,
                               &jobs[d].dev, c->stream, shared ? &rays[base[d]].origin : NULL))
             return -1;
     }
@@ -1706,20 +1710,40 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                 const Ray* src = rays + d0s[d];
                 const long nbk = (m + BHRT_BATCH_BLOCK - 1) / BHRT_BATCH_BLOCK;
                 const Vector3D o = src[0].origin;
-                int diff = 0; /* does any ray of the chunk start elsewhere than src[0]? */
+                /* rays that all start at src[0]'s origin travel as their directions alone
+                 * (24 of 48 bytes: the upload before the chunk can start is halved); a chunk
+                 * with any other origin is staged again whole */
+                int diff = !env_int("BHRT_SHARED_ORIGIN", 1);
+                double* hd = (double*)hr;
+                if (!diff) {
 #pragma omp parallel for schedule(static) reduction(| : diff) num_threads(stage_threads) if (nbk >= 4)
-                for (long j = 0; j < nbk; j++) { /* local block j = device block plan_block() */
-                    const long b0 = plan_block(&P, k, j) * BHRT_BATCH_BLOCK;
-                    const long len = md - b0 < BHRT_BATCH_BLOCK ? md - b0 : BHRT_BATCH_BLOCK;
-                    Ray* dst = hr + j * BHRT_BATCH_BLOCK;
-                    memcpy(dst, src + b0, (size_t)len * sizeof(Ray));
-                    for (long i = 0; i < len; i++) /* (the block is in cache after the copy) */
-                        diff |= memcmp(&dst[i].origin, &o, sizeof o) != 0;
+                    for (long j = 0; j < nbk; j++) { /* local block j = device block plan_block() */
+                        const long b0 = plan_block(&P, k, j) * BHRT_BATCH_BLOCK;
+                        const long len = md - b0 < BHRT_BATCH_BLOCK ? md - b0 : BHRT_BATCH_BLOCK;
+                        double* dst = hd + 3 * j * BHRT_BATCH_BLOCK;
+                        for (long i = 0; i < len; i++) {
+                            const Ray* r = &src[b0 + i];
+                            diff |= memcmp(&r->origin, &o, sizeof o) != 0;
+                            dst[3 * i] = r->direction.x;
+                            dst[3 * i + 1] = r->direction.y;
+                            dst[3 * i + 2] = r->direction.z;
+                        }
+                    }
                 }
-                HIP_TRY(hipMemcpyAsync((Ray*)c->d_rays + a, hr, (size_t)m * sizeof(Ray),
-                                       hipMemcpyHostToDevice, st));
-                if (trace_rays_device((const Ray*)c->d_rays + a, (int)m, bh, dk, cfg,
-                                      INTEGRATOR_RK4, 0, &jobs[k][d].dev, st, diff ? NULL : &o))
+                if (diff) {
+#pragma omp parallel for schedule(static) num_threads(stage_threads) if (nbk >= 4)
+                    for (long j = 0; j < nbk; j++) {
+                        const long b0 = plan_block(&P, k, j) * BHRT_BATCH_BLOCK;
+                        const long len = md - b0 < BHRT_BATCH_BLOCK ? md - b0 : BHRT_BATCH_BLOCK;
+                        memcpy(hr + j * BHRT_BATCH_BLOCK, src + b0, (size_t)len * sizeof(Ray));
+                    }
+                }
+                const size_t bytes = (size_t)m * (diff ? sizeof(Ray) : 3 * sizeof(double));
+                HIP_TRY(hipMemcpyAsync((Ray*)c->d_rays + a, hr, bytes, hipMemcpyHostToDevice, st));
+                const Ray* dr = (const Ray*)c->d_rays + a;
+                if (trace_rays_device(diff ? dr : NULL, diff ? NULL : (const double*)dr, (int)m,
+                                      bh, dk, cfg, INTEGRATOR_RK4, 0, &jobs[k][d].dev, st,
+                                      diff ? NULL : &o))
                     return -1;
             }
             HIP_TRY(hipEventRecord(c->chunk_done[k], st));

@@ -117,6 +117,10 @@ typedef struct {
     int rays_shared;      /* BHRT_SRC_RAYS whose every origin is cam.pos (the host checked):
                              cam's origin block is filled as for a camera frame, and the
                              trace kernel sets rays up from their directions (no k_init) */
+    const double* dirs;   /* rays_shared: ray i's direction at dirs[i * dir_stride + 0..2]
+                             (the AoS rays' direction field, stride 6, or packed, stride 3,
+                             with rays NULL) */
+    int dir_stride;
 } bhrt_kparams;
 
 /* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and

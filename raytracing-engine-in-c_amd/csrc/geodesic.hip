@@ -815,11 +815,12 @@ __device__ __forceinline__ void ray_init_camera(Ray_& R, const bhrt_camera_k& cm
 // origin part of the set-up is the host's (cm, as for a camera frame); the direction is the
 // array's, kept as given for the disk test (Ray.direction) and normalised for the velocities,
 // as ray_init_general does.
-__device__ __forceinline__ void ray_init_shared(Ray_& R, const bhrt_camera_k& cm, const Ray* rays,
-                                                int i) {
-    R.dx = rays[i].direction.x;
-    R.dy = rays[i].direction.y;
-    R.dz = rays[i].direction.z;
+__device__ __forceinline__ void ray_init_shared(Ray_& R, const bhrt_camera_k& cm,
+                                                const double* dirs, int stride, int i) {
+    const double* d = dirs + (size_t)i * stride;
+    R.dx = d[0];
+    R.dy = d[1];
+    R.dz = d[2];
     double nx, ny, nz;
     normalize3(R.dx, R.dy, R.dz, nx, ny, nz);
     init_velocity(R, nx, ny, nz, cm.r0, cm.st_cp, cm.st_sp, cm.ct, cm.ct_cp, cm.ct_sp, cm.st,
@@ -1328,7 +1329,14 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
             f[6 * n + i] = R.dz;
             f[7 * n + i] = R.far_ok ? 1.0 : 0.0;
         } else {
-            const Ray ray = kp.rays[i];
+            Ray ray;
+            if (kp.rays_shared) {  // the origin block's point, the packed or AoS direction
+                const double* d = kp.dirs + (size_t)i * kp.dir_stride;
+                ray.origin = Vector3D{kp.cam.pos[0], kp.cam.pos[1], kp.cam.pos[2]};
+                ray.direction = Vector3D{d[0], d[1], d[2]};
+            } else {
+                ray = kp.rays[i];
+            }
             ray_init_general(R, 0.0, ray.origin.x, ray.origin.y, ray.origin.z, ray.direction.x,
                              ray.direction.y, ray.direction.z, kp.sc);
 #pragma unroll
@@ -1546,7 +1554,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     // (the redo list holds ray ids; the k_init table is in claim order)
                     if (INL || (HUGE && (kp.order || kp.cam.tiles_per_row))) {
                         if constexpr (INL == 2)
-                            ray_init_shared(R, kc.cam, kc.rays, rid);
+                            ray_init_shared(R, kc.cam, kc.dirs, kc.dir_stride, rid);
                         else
                             ray_init_camera(R, kc.cam, rid);
                         R.s1 = as1;
@@ -1652,6 +1660,11 @@ __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
         double dx, dy, dz;
         if (SRC == BHRT_SRC_CAMERA) {
             camera_dir(kp.cam, i, dx, dy, dz);
+        } else if (kp.rays_shared) {
+            const double* d = kp.dirs + (size_t)i * kp.dir_stride;
+            dx = d[0];
+            dy = d[1];
+            dz = d[2];
         } else {
             dx = kp.rays[i].direction.x;
             dy = kp.rays[i].direction.y;

@@ -59,7 +59,11 @@ int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0, void* ev1
     on_device(kp->ctl, 8 * 8, "control block");
     on_device(kp->qhead, 8, "queue heads");
     on_device(kp->init, (size_t)(BHRT_INIT_FIELDS + 1) * 8 * n, "init table");
-    if (kp->src == BHRT_SRC_RAYS) on_device(kp->rays, sizeof(Ray) * n, "rays");
+    if (kp->src == BHRT_SRC_RAYS && !kp->rays_shared) on_device(kp->rays, sizeof(Ray) * n, "rays");
+    if (kp->src == BHRT_SRC_RAYS && kp->rays_shared) {
+        on_device(kp->dirs, 8 * ((size_t)kp->dir_stride * (n - 1) + 3), "directions");
+        if (kp->rays) on_device(kp->rays, sizeof(Ray) * n, "rays");
+    }
     for (long i = 0; i < n; i++) {
         long v;
         if (kp->src == BHRT_SRC_CAMERA) {
@@ -71,13 +75,13 @@ int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0, void* ev1
             }
             v = py * W + px;
         } else if (kp->rays_shared) { /* one origin (the host said so): the id rides in dx */
-            if (memcmp(&kp->rays[i].origin.x, &kp->cam.pos[0], 8) ||
-                memcmp(&kp->rays[i].origin.y, &kp->cam.pos[1], 8) ||
-                memcmp(&kp->rays[i].origin.z, &kp->cam.pos[2], 8)) {
+            if (kp->rays && (memcmp(&kp->rays[i].origin.x, &kp->cam.pos[0], 8) ||
+                             memcmp(&kp->rays[i].origin.y, &kp->cam.pos[1], 8) ||
+                             memcmp(&kp->rays[i].origin.z, &kp->cam.pos[2], 8))) {
                 fprintf(stderr, "rays_shared launch with a ray off the shared origin\n");
                 abort();
             }
-            v = (long)kp->rays[i].direction.x;
+            v = (long)kp->dirs[(size_t)i * kp->dir_stride];
         } else {
             v = (long)kp->rays[i].origin.x;
         }
