@@ -5,9 +5,11 @@ cd "$(dirname "$0")/.."
 OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
+echo "== torch after libbhrt"
+timeout -k 10 600 python3 tools/torch_after_lib.py || { echo "diag failed"; exit 1; }
 echo "== batch tests"
 for w in "" "1,3,3,1"; do
-  BHRT_BATCH_WEIGHTS="$w" timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread -k "batch or shared_origin or rays" > $OUT/pytest_batch_k.log 2>&1 \
+  BHRT_BATCH_WEIGHTS="$w" timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread -k "batch or shared_origin or rays_vs" > $OUT/pytest_batch_k.log 2>&1 \
     || { echo "pytest failed"; tail -30 $OUT/pytest_batch_k.log; exit 1; }
   tail -1 $OUT/pytest_batch_k.log
 done
