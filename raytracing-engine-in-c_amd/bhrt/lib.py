@@ -94,6 +94,19 @@ _PROTOS = {
 }
 
 
+def _one_hip_runtime():
+    """Import torch (if installed) before libbhrt is mapped. The torch wheel carries its own HIP
+    runtime, torch/lib/libamdhip64.so, whose SONAME is libamdhip64.so.7 -- the name libbhrt.so
+    needs. Loaded first, it is the process's one runtime and libbhrt binds to it (torch's device
+    buffers and streams are then libbhrt's too). Loaded after libbhrt, torch -- which needs the
+    library by its file name -- maps a second runtime next to /opt/rocm's, and its device
+    initialisation fails ("No HIP GPUs are available", tools/torch_after_lib.py)."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load(path=None):
     """Load libbhrt.so once; raise BhrtError (never fall back) if it is not there."""
     global _lib
@@ -102,6 +115,7 @@ def load(path=None):
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise BhrtError(f"libbhrt.so not built at {p} (run __graft_entry__.build())")
+    _one_hip_runtime()
     lib = C.CDLL(p)
     older = p != _DEFAULT_PATH  # an A/B build of an earlier revision may lack newer entry points
     for name, (res, args) in _PROTOS.items():

@@ -9,11 +9,12 @@
 Tolerance: integers (class, steps) bit-exact; floats 1e-5 relative (BASELINE north_star).
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
 
-from conftest import (camera_from, compare, fixture_outputs, full_frame_report, golden,
+from conftest import (ROOT, camera_from, compare, fixture_outputs, full_frame_report, golden,
                       golden_names, rays_from, scene_from, sky_pinned)
 from bhrt import abi, configs
 
@@ -845,6 +846,22 @@ def test_shared_origin_ray_arrays_vs_oracle(bhrt_lib, oracle, monkeypatch, cname
     monkeypatch.setenv("BHRT_SHARED_ORIGIN", "0")
     gen = bhrt_lib.trace_rays(rays, bh, dk, cfg, c.method, c.flags)
     compare(gen, want, RTOL, sky_pinned(c.method), f"{cname} per-ray set-up")
+
+
+def test_torch_after_libbhrt_in_a_fresh_process():
+    """A process that loads libbhrt before it first uses torch on the GPU still has ONE HIP
+    runtime (bhrt.lib imports torch before mapping libbhrt: torch's bundled libamdhip64 then
+    serves both), so torch's device initialisation works and its buffers go to libbhrt."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from bhrt import lib\n"
+            "assert lib.load().bhrt_device_count() > 0\n"
+            "import torch\n"
+            "t = torch.zeros(8, device='cuda'); torch.cuda.synchronize(); print('ok', t.sum().item())\n"
+            % str(os.path.join(ROOT, "raytracing-engine-in-c_amd")))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok 0.0" in r.stdout, r.stderr[-2000:]
 
 
 def test_rkf45_accept_band(bhrt_lib):
