@@ -100,7 +100,10 @@ def _one_hip_runtime():
     needs. Loaded first, it is the process's one runtime and libbhrt binds to it (torch's device
     buffers and streams are then libbhrt's too). Loaded after libbhrt, torch -- which needs the
     library by its file name -- maps a second runtime next to /opt/rocm's, and its device
-    initialisation fails ("No HIP GPUs are available", tools/torch_after_lib.py)."""
+    initialisation fails ("No HIP GPUs are available", tools/torch_after_lib.py).
+    BHRT_PY_NO_TORCH=1 skips it (a torch-free process then runs /opt/rocm's runtime)."""
+    if os.environ.get("BHRT_PY_NO_TORCH") == "1":
+        return
     try:
         import torch  # noqa: F401
     except ImportError:
