@@ -1,6 +1,6 @@
 """trace_rays_batch (the reference's batch API: Ray[] in, RayTraceHit[] out) for the C2
 camera's 2 M rays: wall time per call with reused arrays, against the trace kernel, for several
-chunk counts (BHRT_HOST_CHUNKS) and pack thread counts; BHRT_HOST_TIMING=1 adds libbhrt's
+chunk counts (BHRT_HOST_CHUNKS; "x" = the default plan) and pack thread counts; BHRT_HOST_TIMING=1 adds libbhrt's
 per-call breakdown (staging + issue, waiting for chunks, packing) on stderr."""
 import ctypes as C
 import os
@@ -22,7 +22,10 @@ hits = np.zeros(W * H, dtype=abi.HIT_DTYPE)
 L = lib.load()
 for chunks in os.environ.get("CHUNKS", "4 2 3 6 8").split():
     for threads in (0, 8):
-        os.environ["BHRT_HOST_CHUNKS"] = chunks
+        if chunks == "x":  # the library's default plan
+            os.environ.pop("BHRT_HOST_CHUNKS", None)
+        else:
+            os.environ["BHRT_HOST_CHUNKS"] = chunks
         args = (rays.ctypes.data, W * H, C.byref(bh), C.byref(dk), C.byref(cfg),
                 hits.ctypes.data, threads)
         assert L.trace_rays_batch(*args) == 0
