@@ -20,6 +20,15 @@ W, H = 1920, 1080
 rays = configs.camera_rays(cam, W, H)
 hits = np.zeros(W * H, dtype=abi.HIT_DTYPE)
 L = lib.load()
+# PRE_STREAMS=k: k torch streams created and used first (as bench.py's frame streams are), to see
+# whether libbhrt's own streams then share hardware queues with busy or idle streams
+if int(os.environ.get("PRE_STREAMS", "0")):
+    import torch
+    ss = [torch.cuda.Stream() for _ in range(int(os.environ["PRE_STREAMS"]))]
+    for st in ss:
+        with torch.cuda.stream(st):
+            torch.zeros(1024, device="cuda").add_(1)
+    torch.cuda.synchronize()
 for chunks in os.environ.get("CHUNKS", "4 2 3 6 8").split():
     for threads in (0, 8):
         if chunks == "x":  # the library's default plan
