@@ -324,6 +324,36 @@ static int ensure(void** p, size_t* cap, size_t need, int pinned);
  * a caller that only drives the device API on its own streams (bench.py) never creates them,
  * so they take none of the process's hardware queues (GPU_MAX_HW_QUEUES; streams beyond it
  * share a queue, and work on a shared queue runs in order) */
+/* One of libbhrt's own streams (device current). Every stream is bound to a hardware queue
+ * (GPU_MAX_HW_QUEUES per process, assigned round robin over the process's streams), and work on
+ * one queue runs in order: if the two trace streams of a ray batch, or a trace stream and the
+ * copy stream, land on one queue, chunk k + 1 cannot fill chunk k's tail and a chunk's download
+ * waits for the next chunk's trace. Which queue a plain stream gets depends on how many streams
+ * the process made before (torch's: trace_rays_batch ran 144 instead of 200 Mrays/s after two
+ * torch streams, profiles/r04/session_p). BHRT_STREAM_QUEUE: 0 = plain non-blocking stream,
+ * 1 = the greatest stream priority (a queue of that priority), 2 = a full CU mask (a queue of
+ * its own). */
+static int own_stream(hipStream_t* s) {
+    const int mode = env_int("BHRT_STREAM_QUEUE", 0);
+    if (mode == 1) {
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+            return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi) == hipSuccess ? 0 : -1;
+    } else if (mode == 2) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            cus > 0 && cus <= 1024) {
+            uint32_t mask[32];
+            const int words = (cus + 31) / 32;
+            for (int i = 0; i < words; i++)
+                mask[i] = (i == words - 1 && cus % 32) ? (1u << (cus % 32)) - 1u : 0xffffffffu;
+            return hipExtStreamCreateWithCUMask(s, (uint32_t)words, mask) == hipSuccess ? 0 : -1;
+        }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess ? 0 : -1;
+}
+
 static int ctx_streams(devctx_t* c) {
     if (c->stream && c->stream2 && c->copy) return 0;
     int cur = -1;
@@ -333,9 +363,8 @@ static int ctx_streams(devctx_t* c) {
             return -1;
         }
     }
-    if ((!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) ||
-        (!c->stream2 && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) ||
-        (!c->copy && hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess)) {
+    if ((!c->stream && own_stream(&c->stream)) || (!c->stream2 && own_stream(&c->stream2)) ||
+        (!c->copy && own_stream(&c->copy))) {
         set_err("cannot create libbhrt's streams on device %d", c->device);
         if (cur >= 0 && cur != c->device) (void)hipSetDevice(cur);
         return -1;
@@ -1690,7 +1719,10 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
         HIP_TRY(hipSetDevice(d));
         if (ctx_streams(c)) return -1;
         for (int i = 0; i + 2 < nst; i++)
-            if (!c->xs[i]) HIP_TRY(hipStreamCreateWithFlags(&c->xs[i], hipStreamNonBlocking));
+            if (!c->xs[i] && own_stream(&c->xs[i])) {
+                set_err("cannot create a trace stream on device %d", d);
+                return -1;
+            }
         const long m = ms[d];
         if (ensure(&c->d_rays, &c->cap_rays, (size_t)m * sizeof(Ray), 0) ||
             ensure(&c->d_soa, &c->cap_soa, (size_t)m * HIT_BYTES + 4096 * K, 0) ||

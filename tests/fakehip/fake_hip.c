@@ -203,6 +203,25 @@ hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned flags) {
     (*s)->dev = g_dev;
     return hipSuccess;
 }
+hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t a, int dev) {
+    (void)dev;
+    *v = a == hipDeviceAttributeMultiprocessorCount ? 256 : 0;
+    return hipSuccess;
+}
+hipError_t hipStreamCreateWithPriority(hipStream_t* s, unsigned flags, int priority) {
+    (void)priority;
+    return hipStreamCreateWithFlags(s, flags);
+}
+hipError_t hipDeviceGetStreamPriorityRange(int* lo, int* hi) {
+    *lo = 0;
+    *hi = -1;
+    return hipSuccess;
+}
+hipError_t hipExtStreamCreateWithCUMask(hipStream_t* s, uint32_t n, const uint32_t* mask) {
+    (void)n;
+    (void)mask;
+    return hipStreamCreateWithFlags(s, 0);
+}
 hipError_t hipStreamSynchronize(hipStream_t s) {
     check_stream(s);
     return hipSuccess;

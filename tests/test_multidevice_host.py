@@ -50,8 +50,11 @@ def test_two_simulated_devices_asan_ubsan(tmp_path):
     env = {"ASAN_OPTIONS": "detect_leaks=0", "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}
     # the default chunk plan, and trace_rays_batch's weighted plans (BHRT_BATCH_WEIGHTS: small
     # first and last chunks, chunk counts 2..8)
-    for weights in (None, "1,5,5,4,1", "3,1", "1,2,3,4,5,6,7,8"):
-        extra = {"BHRT_BATCH_WEIGHTS": weights} if weights else {}
+    # (and libbhrt's streams made each way BHRT_STREAM_QUEUE offers)
+    for weights, queue in ((None, "0"), ("1,5,5,4,1", "1"), ("3,1", "2"), ("1,2,3,4,5,6,7,8", "0")):
+        extra = {"BHRT_STREAM_QUEUE": queue}
+        if weights:
+            extra["BHRT_BATCH_WEIGHTS"] = weights
         r = run(exe, **env, **extra)
         assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
 
