@@ -39,6 +39,8 @@ def main():
     ap.add_argument("copies")
     ap.add_argument("--gap", type=float, default=0.5, help="idle gap (ms) that separates calls")
     ap.add_argument("--call", type=int, default=-1, help="which call with trace kernels (-1: last)")
+    ap.add_argument("--min-span", type=float, default=0.0,
+                    help="only calls at least this long (ms): skips trace_ray calls after a batch")
     a = ap.parse_args()
     ev = []
     with open(a.kernels) as f:
@@ -60,7 +62,8 @@ def main():
         cur.append(e)
         end = e[1] if end is None else max(end, e[1])
     calls.append(cur)
-    calls = [c for c in calls if any(n.startswith("k_trace") for _, _, _, n in c)]
+    calls = [c for c in calls if any(n.startswith("k_trace") for _, _, _, n in c) and
+             (max(e for _, e, _, _ in c) - c[0][0]) / 1e6 >= a.min_span]
     last = calls[a.call]
     t0 = last[0][0]
     for s, e, k, n in last:
