@@ -29,6 +29,13 @@ if int(os.environ.get("PRE_STREAMS", "0")):
         with torch.cuda.stream(st):
             torch.zeros(1024, device="cuda").add_(1)
     torch.cuda.synchronize()
+# PRE_FRAMES=k: k synchronous host-buffer frames (every field) of the same camera first, as
+# bench.py's host-path leg renders before its batch calls
+if int(os.environ.get("PRE_FRAMES", "0")):
+    arrays, soa = abi.alloc_soa(W * H, abi.SOA_FIELDS)
+    for _ in range(int(os.environ["PRE_FRAMES"])):
+        assert L.bhrt_render_frame(C.byref(bh), C.byref(dk), C.byref(cfg), C.byref(cam), W, H,
+                                   c.method, c.flags, C.byref(soa)) == 0
 for chunks in os.environ.get("CHUNKS", "4 2 3 6 8").split():
     for threads in (0, 8):
         if chunks == "x":  # the library's default plan
