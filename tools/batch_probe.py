@@ -36,6 +36,15 @@ if int(os.environ.get("PRE_FRAMES", "0")):
     for _ in range(int(os.environ["PRE_FRAMES"])):
         assert L.bhrt_render_frame(C.byref(bh), C.byref(dk), C.byref(cfg), C.byref(cam), W, H,
                                    c.method, c.flags, C.byref(soa)) == 0
+if os.environ.get("WHERE"):  # the CPU (and its NUMA node) this process runs on, per call
+    import glob
+
+    def where():
+        cpu = int(open("/proc/self/stat").read().rsplit(")", 1)[1].split()[36])
+        node = [d.rsplit("node", 1)[1] for d in glob.glob(f"/sys/devices/system/cpu/cpu{cpu}/node*")]
+        return f"cpu {cpu} node {','.join(node)}"
+    gpus = sorted({open(f).read().strip() for f in glob.glob("/sys/class/drm/renderD*/device/numa_node")})
+    print("gpu numa nodes", gpus, "affinity", len(os.sched_getaffinity(0)), "cpus", flush=True)
 for chunks in os.environ.get("CHUNKS", "4 2 3 6 8").split():
     for threads in (0, 8):
         if chunks == "x":  # the library's default plan
@@ -51,6 +60,8 @@ for chunks in os.environ.get("CHUNKS", "4 2 3 6 8").split():
             assert L.trace_rays_batch(*args) == 0
         dt = (time.perf_counter() - t) / 4
         st = lib.stats(reset=True)
+        if os.environ.get("WHERE"):
+            print(where(), flush=True)
         print(f"trace_rays_batch 2M rays, {chunks} chunks, num_threads {threads}: "
               f"{dt * 1e3:.2f} ms/call ({W * H / dt / 1e6:.1f} Mrays/s), kernel "
               f"{st['kernel_ms'] / 4:.2f} ms/call over {st['launches'] // 4} launches", flush=True)
