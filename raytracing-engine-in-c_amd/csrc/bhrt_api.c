@@ -331,10 +331,11 @@ static int ensure(void** p, size_t* cap, size_t need, int pinned);
  * waits for the next chunk's trace. Which queue a plain stream gets depends on how many streams
  * the process made before (torch's: trace_rays_batch ran 144 instead of 200 Mrays/s after two
  * torch streams, profiles/r04/session_p). BHRT_STREAM_QUEUE: 0 = plain non-blocking stream,
- * 1 = the greatest stream priority (a queue of that priority), 2 = a full CU mask (a queue of
- * its own). */
+ * 1 = the greatest stream priority (default: queues of that priority, which only libbhrt's
+ * streams use -- 146 -> 204 Mrays/s in that case, neutral elsewhere, profiles/r04/session_q),
+ * 2 = a full CU mask (a queue of its own). */
 static int own_stream(hipStream_t* s) {
-    const int mode = env_int("BHRT_STREAM_QUEUE", 0);
+    const int mode = env_int("BHRT_STREAM_QUEUE", 1);
     if (mode == 1) {
         int lo = 0, hi = 0;
         if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
