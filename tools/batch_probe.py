@@ -45,6 +45,31 @@ if os.environ.get("WHERE"):  # the CPU (and its NUMA node) this process runs on,
         return f"cpu {cpu} node {','.join(node)}"
     gpus = sorted({open(f).read().strip() for f in glob.glob("/sys/class/drm/renderD*/device/numa_node")})
     print("gpu numa nodes", gpus, "affinity", len(os.sched_getaffinity(0)), "cpus", flush=True)
+# PRE_ASYNC=k: k host-buffer frames three in flight (bhrt_render_frame_async, bench.py's async leg)
+if int(os.environ.get("PRE_ASYNC", "0")):
+    sets = [abi.alloc_soa(W * H, abi.SOA_FIELDS) for _ in range(3)]
+    tickets = []
+    for i in range(int(os.environ["PRE_ASYNC"])):
+        t = C.c_int(0)
+        assert L.bhrt_render_frame_async(C.byref(bh), C.byref(dk), C.byref(cfg), C.byref(cam), W,
+                                         H, c.method, c.flags, C.byref(sets[i % 3][1]),
+                                         C.byref(t)) == 0
+        tickets.append(t.value)
+        if len(tickets) == 3:
+            assert L.bhrt_frame_wait(tickets.pop(0)) == 0
+    for t in tickets:
+        assert L.bhrt_frame_wait(t) == 0
+# PRE_DEVICE=k: k device frames on two torch streams (bench.py's timed frames)
+if int(os.environ.get("PRE_DEVICE", "0")):
+    import torch
+    ss = [torch.cuda.Stream() for _ in range(2)]
+    bufs = [{f: torch.zeros(W * H, dtype=torch.int32 if f in ("result", "steps") else
+                            torch.float64, device="cuda") for f in abi.SOA_FIELDS} for _ in ss]
+    for i in range(int(os.environ["PRE_DEVICE"])):
+        st = ss[i % 2]
+        lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                lib.soa_from_tensors(bufs[i % 2]), st.cuda_stream)
+    torch.cuda.synchronize()
 for chunks in os.environ.get("CHUNKS", "4 2 3 6 8").split():
     for threads in (0, 8):
         if chunks == "x":  # the library's default plan
