@@ -136,6 +136,9 @@ typedef struct {
      * copy stream, and per chunk: trace finished / its D2H landed */
     hipStream_t stream2, copy;
     hipStream_t xs[2]; /* trace streams 3 and 4 of pipelined ray batches (created on first use) */
+    hipEvent_t tev[BHRT_MAX_CHUNKS][4]; /* BHRT_HOST_TIMING=2: per batch chunk, timing events
+                                           (upload issued, uploaded, traced, downloaded) */
+    hipEvent_t tev0;
     hipEvent_t chunk_done[BHRT_MAX_CHUNKS], chunk_copied[BHRT_MAX_CHUNKS];
     /* per frame slot of bhrt_render_frame_async: device SoA of every chunk, pinned staging
      * of the caller's fields, chunk traced / chunk copied */
@@ -1697,6 +1700,7 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
     if (env && atoi(env) >= 1 && atoi(env) <= BHRT_MAX_CHUNKS) K = atoi(env);
     const int stage_threads = host_threads();
     const int timing = getenv("BHRT_HOST_TIMING") != NULL;
+    const int tl = env_int("BHRT_HOST_TIMING", 0) == 2; /* + each chunk's GPU timeline */
     /* trace streams the chunks rotate over (BHRT_BATCH_STREAMS): 2 -- with 4, every chunk
      * queued at once, C2 camera rays ran 158 instead of 172 Mrays/s (profiles/r04) */
     int nst = env_int("BHRT_BATCH_STREAMS", 2);
@@ -1725,6 +1729,12 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                 return -1;
             }
         const long m = ms[d];
+        if (tl && !c->tev0) {
+            HIP_TRY(hipEventCreate(&c->tev0));
+            for (int k = 0; k < BHRT_MAX_CHUNKS; k++)
+                for (int e = 0; e < 4; e++) HIP_TRY(hipEventCreate(&c->tev[k][e]));
+        }
+        if (tl) HIP_TRY(hipEventRecord(c->tev0, c->stream));
         if (ensure(&c->d_rays, &c->cap_rays, (size_t)m * sizeof(Ray), 0) ||
             ensure(&c->d_soa, &c->cap_soa, (size_t)m * HIT_BYTES + 4096 * K, 0) ||
             ensure(&c->h_rays, &c->cap_hrays, (size_t)m * sizeof(Ray), 1) ||
@@ -1775,7 +1785,9 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                     }
                 }
                 const size_t bytes = (size_t)m * (diff ? sizeof(Ray) : 3 * sizeof(double));
+                if (tl) HIP_TRY(hipEventRecord(c->tev[k][0], st));
                 HIP_TRY(hipMemcpyAsync((Ray*)c->d_rays + a, hr, bytes, hipMemcpyHostToDevice, st));
+                if (tl) HIP_TRY(hipEventRecord(c->tev[k][1], st));
                 const Ray* dr = (const Ray*)c->d_rays + a;
                 if (trace_rays_device(diff ? dr : NULL, diff ? NULL : (const double*)dr, (int)m,
                                       bh, dk, cfg, INTEGRATOR_RK4, 0, &jobs[k][d].dev, st,
@@ -1783,12 +1795,14 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                     return -1;
             }
             HIP_TRY(hipEventRecord(c->chunk_done[k], st));
+            if (tl) HIP_TRY(hipEventRecord(c->tev[k][2], st));
             HIP_TRY(hipStreamWaitEvent(c->copy, c->chunk_done[k], 0));
             if (m > 0) /* device and staging chunks share hit_fields' layout: one copy */
                 HIP_TRY(hipMemcpyAsync((char*)c->h_stage + (size_t)a * HIT_BYTES,
                                        jobs[k][d].dev.result, (size_t)m * HIT_BYTES,
                                        hipMemcpyDeviceToHost, c->copy));
             HIP_TRY(hipEventRecord(c->chunk_copied[k], c->copy));
+            if (tl) HIP_TRY(hipEventRecord(c->tev[k][3], c->copy));
         }
     clock_gettime(CLOCK_MONOTONIC, &tt[1]);
     double wait_ms = 0.0, pack_ms = 0.0;
@@ -1823,6 +1837,16 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                 "pack %.2f ms (%d threads)\n", n, K,
                 (tt[1].tv_sec - tt[0].tv_sec) * 1e3 + (tt[1].tv_nsec - tt[0].tv_nsec) * 1e-6,
                 wait_ms, pack_ms, nthreads);
+    if (tl) /* device 0's chunks: upload start / end, traced, downloaded (ms after the call) */
+        for (int k = 0; k < K; k++) {
+            devctx_t* c = jobs[k][0].c;
+            float t[4] = {0, 0, 0, 0};
+            for (int e = 0; e < 4; e++)
+                if (jobs[k][0].n > 0 || e >= 2)
+                    (void)hipEventElapsedTime(&t[e], c->tev0, c->tev[k][e]);
+            fprintf(stderr, "  chunk %d (%ld rays): upload %.3f-%.3f traced %.3f downloaded %.3f\n",
+                    k, jobs[k][0].n, t[0], t[1], t[2], t[3]);
+        }
     return 0;
 }
 
