@@ -478,12 +478,14 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
         dta = (time.perf_counter() - t0) / frames
         return dt, dta, sum(a.nbytes for a in sets[0][0].values())
 
-    dt, dta, nbytes = leg(FIELDS)
-    dt8, dta8, nbytes8 = leg(("rgba8",))
     # the reference's batch API (trace_rays_batch: Ray[] in, 160-byte RayTraceHit[] out, only
-    # the fields trace_ray writes) on the frame's camera rays, arrays reused
-    batch = None
-    if c.method == abi.INTEGRATOR_RK4:  # (trace_rays_batch is trace_ray, RK4)
+    # the fields trace_ray writes) on the frame's camera rays, arrays reused -- measured before
+    # the host-frame legs (what a caller of this API alone sees) and again after them: calls that
+    # follow host-buffer frames in the same process are often ~30% slower, GPU-side, for a
+    # reason not found ("Host-buffer ray batches")
+    def batch_rate():
+        if c.method != abi.INTEGRATOR_RK4:  # (trace_rays_batch is trace_ray, RK4)
+            return None
         rays = configs.camera_rays(cam, W, H)
         hits = np.zeros(W * H, dtype=abi.HIT_DTYPE)
         bargs = (rays.ctypes.data, W * H, C.byref(bh), C.byref(dk) if dk else None, C.byref(cfg),
@@ -493,7 +495,12 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
         t0 = time.perf_counter()
         for _ in range(3):
             L.trace_rays_batch(*bargs)
-        batch = round(W * H / ((time.perf_counter() - t0) / 3) / 1e6, 3)
+        return round(W * H / ((time.perf_counter() - t0) / 3) / 1e6, 3)
+
+    batch = batch_rate()
+    dt, dta, nbytes = leg(FIELDS)
+    dt8, dta8, nbytes8 = leg(("rgba8",))
+    batch_after = batch_rate()
     # one drop-in trace_ray call (the camera's forward ray), host round trip included
     ray = abi.Ray(cam.position, cam.direction)
     hit = abi.RayTraceHit()
@@ -513,12 +520,14 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
             "rgba8_async_mrays_s": round(W * H / dta8 / 1e6, 3),
             "rgba8_bytes_to_host_per_frame": nbytes8,
             "trace_rays_batch_mrays_s": batch,
+            "trace_rays_batch_after_frames_mrays_s": batch_after,
             "trace_ray_latency_ms": round(sorted(lat[2:])[len(lat[2:]) // 2] * 1e3, 3),
             "note": "bhrt_render_frame into reused host arrays (every field; pinned staging, "
                     "host un-permute by up to 16 threads); async = bhrt_render_frame_async with "
                     "three frames in flight; rgba8 = the same calls with only the display buffer "
                     "(the visualizer's call, INTEGRATION.md); trace_rays_batch = the reference "
-                    "batch API on the frame's camera rays (RayTraceHit[] out); trace_ray = median "
+                    "batch API on the frame's camera rays (RayTraceHit[] out), measured before "
+                    "the host-frame legs and again after them; trace_ray = median "
                     "of one drop-in call, PCIe round trip included"}
 
 
