@@ -480,9 +480,9 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
 
     # the reference's batch API (trace_rays_batch: Ray[] in, 160-byte RayTraceHit[] out, only
     # the fields trace_ray writes) on the frame's camera rays, arrays reused -- measured before
-    # the host-frame legs (what a caller of this API alone sees) and again after them: calls that
-    # follow host-buffer frames in the same process are often ~30% slower, GPU-side, for a
-    # reason not found ("Host-buffer ray batches")
+    # the host-frame legs and again after them. In this process both read ~30% below a fresh
+    # process's calls (tools/batch_probe.py), GPU-side, for a reason not found (DESIGN.md
+    # section 4, "Host-buffer ray batches")
     def batch_rate():
         if c.method != abi.INTEGRATOR_RK4:  # (trace_rays_batch is trace_ray, RK4)
             return None
