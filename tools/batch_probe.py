@@ -70,6 +70,19 @@ if int(os.environ.get("PRE_DEVICE", "0")):
         lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
                                 lib.soa_from_tensors(bufs[i % 2]), st.cuda_stream)
     torch.cuda.synchronize()
+# PRE_PIN=MB: a pinned host buffer of that size allocated (and freed unless PRE_PIN_KEEP=1) first
+if int(os.environ.get("PRE_PIN", "0")):
+    import torch
+    pinned = torch.empty(int(os.environ["PRE_PIN"]) << 20, dtype=torch.uint8, pin_memory=True)
+    pinned.fill_(1)
+    if os.environ.get("PRE_PIN_KEEP") != "1":
+        del pinned
+# PRE_PAGEABLE=k: k pageable device-to-host torch copies of a 200 MB tensor first
+if int(os.environ.get("PRE_PAGEABLE", "0")):
+    import torch
+    t = torch.ones(25 << 20, dtype=torch.float64, device="cuda")
+    for _ in range(int(os.environ["PRE_PAGEABLE"])):
+        t.cpu()
 for chunks in os.environ.get("CHUNKS", "4 2 3 6 8").split():
     for threads in (0, 8):
         if chunks == "x":  # the library's default plan
