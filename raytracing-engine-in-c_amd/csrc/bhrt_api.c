@@ -1701,6 +1701,9 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
     const int stage_threads = host_threads();
     const int timing = getenv("BHRT_HOST_TIMING") != NULL;
     const int tl = env_int("BHRT_HOST_TIMING", 0) == 2; /* + each chunk's GPU timeline */
+    /* timing events recorded (bit 0: before a chunk's upload, 1: after it, 2: after its trace,
+     * 3: after its download, 4: at the call's start); BHRT_HOST_TIMING=2 records all */
+    const int mk = tl ? 31 : env_int("BHRT_BATCH_MARKERS", 0);
     /* trace streams the chunks rotate over (BHRT_BATCH_STREAMS): 2 -- with 4, every chunk
      * queued at once, C2 camera rays ran 158 instead of 172 Mrays/s (profiles/r04) */
     int nst = env_int("BHRT_BATCH_STREAMS", 2);
@@ -1729,12 +1732,12 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                 return -1;
             }
         const long m = ms[d];
-        if (tl && !c->tev0) {
+        if (mk && !c->tev0) {
             HIP_TRY(hipEventCreate(&c->tev0));
             for (int k = 0; k < BHRT_MAX_CHUNKS; k++)
                 for (int e = 0; e < 4; e++) HIP_TRY(hipEventCreate(&c->tev[k][e]));
         }
-        if (tl) HIP_TRY(hipEventRecord(c->tev0, c->stream));
+        if (mk & 16) HIP_TRY(hipEventRecord(c->tev0, c->stream));
         if (ensure(&c->d_rays, &c->cap_rays, (size_t)m * sizeof(Ray), 0) ||
             ensure(&c->d_soa, &c->cap_soa, (size_t)m * HIT_BYTES + 4096 * K, 0) ||
             ensure(&c->h_rays, &c->cap_hrays, (size_t)m * sizeof(Ray), 1) ||
@@ -1785,9 +1788,9 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                     }
                 }
                 const size_t bytes = (size_t)m * (diff ? sizeof(Ray) : 3 * sizeof(double));
-                if (tl) HIP_TRY(hipEventRecord(c->tev[k][0], st));
+                if (mk & 1) HIP_TRY(hipEventRecord(c->tev[k][0], st));
                 HIP_TRY(hipMemcpyAsync((Ray*)c->d_rays + a, hr, bytes, hipMemcpyHostToDevice, st));
-                if (tl) HIP_TRY(hipEventRecord(c->tev[k][1], st));
+                if (mk & 2) HIP_TRY(hipEventRecord(c->tev[k][1], st));
                 const Ray* dr = (const Ray*)c->d_rays + a;
                 if (trace_rays_device(diff ? dr : NULL, diff ? NULL : (const double*)dr, (int)m,
                                       bh, dk, cfg, INTEGRATOR_RK4, 0, &jobs[k][d].dev, st,
@@ -1795,14 +1798,14 @@ static int trace_hits_pipelined(const Ray* rays, int n, const BlackHoleParams* b
                     return -1;
             }
             HIP_TRY(hipEventRecord(c->chunk_done[k], st));
-            if (tl) HIP_TRY(hipEventRecord(c->tev[k][2], st));
+            if (mk & 4) HIP_TRY(hipEventRecord(c->tev[k][2], st));
             HIP_TRY(hipStreamWaitEvent(c->copy, c->chunk_done[k], 0));
             if (m > 0) /* device and staging chunks share hit_fields' layout: one copy */
                 HIP_TRY(hipMemcpyAsync((char*)c->h_stage + (size_t)a * HIT_BYTES,
                                        jobs[k][d].dev.result, (size_t)m * HIT_BYTES,
                                        hipMemcpyDeviceToHost, c->copy));
             HIP_TRY(hipEventRecord(c->chunk_copied[k], c->copy));
-            if (tl) HIP_TRY(hipEventRecord(c->tev[k][3], c->copy));
+            if (mk & 8) HIP_TRY(hipEventRecord(c->tev[k][3], c->copy));
         }
     clock_gettime(CLOCK_MONOTONIC, &tt[1]);
     double wait_ms = 0.0, pack_ms = 0.0;
