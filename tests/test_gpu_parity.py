@@ -790,12 +790,18 @@ def test_small_claimed_launches(bhrt_lib, oracle):
         compare(got, want, RTOL, False, f"C4 {W}x{H}")
 
 
-@pytest.mark.parametrize("n", [65536, 300_001, (1 << 20) + 7])  # 4, 4 and 8 chunks
-def test_large_batch_pipelined_equals_soa_trace(bhrt_lib, n):
+@pytest.mark.parametrize("n,weights", [
+    (65536, None), (300_001, None), ((1 << 20) + 7, None),
+    (2_073_600, None),  # the default weighted plan (>= 1 M rays per device)
+    (300_001, "1,1,1,1"), (300_001, "2,5,5,3,1"), (1 << 17, "1,2,3,4,5,6,7,8")])
+def test_large_batch_pipelined_equals_soa_trace(bhrt_lib, monkeypatch, n, weights):
     """trace_rays_batch at n >= 65536 takes the chunked path (rays staged through pinned
     memory, chunks on two trace streams, results packed into RayTraceHit[] by OpenMP
     threads): every hit must equal the one-shot SoA trace of the same rays, and sky_direction
-    must stay untouched for rays that did not escape (raytracer.c:299-333)."""
+    must stay untouched for rays that did not escape (raytracer.c:299-333). Chunk plans
+    (BHRT_BATCH_WEIGHTS) change how rays are dealt over chunks, never the results."""
+    if weights:
+        monkeypatch.setenv("BHRT_BATCH_WEIGHTS", weights)
     rng = np.random.default_rng(n)
     bh, dk, cfg = configs.CONFIGS["C2"].scene()
     rays = np.zeros(n, dtype=abi.RAY_DTYPE)
