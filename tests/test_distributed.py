@@ -29,7 +29,7 @@ def _free_port():
 
 
 def _tiles_worker(rank, world, port, W, H, B, S, gather, frames, cfg_name, max_steps,
-                  out_path):
+                  out_path, slots=2):
     """bench.py's tiles mode: rank r renders shard r of S through FramePipeline, `frames`
     frames in flight through the double-buffered async gathers (frame i = the rendered
     shard with its colour scaled by i + 1, so the frames differ)."""
@@ -49,7 +49,7 @@ def _tiles_worker(rank, world, port, W, H, B, S, gather, frames, cfg_name, max_s
         fields = abi.SOA_FIELDS + (DISPLAY_FIELD if gather == "rgba8" else ())
         pipe = FramePipeline(n, "cpu", world, rank, "shards", H, W, B, fields, shards=S,
                              gather={"all": None, "image": RGB_FIELDS,
-                                     "rgba8": DISPLAY_FIELD}[gather])
+                                     "rgba8": DISPLAY_FIELD}[gather], slots=slots)
         part = orc.oracle().render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags, rows=rows,
                                          threads=2)
         for i in range(frames):
@@ -73,10 +73,11 @@ def _tiles_worker(rank, world, port, W, H, B, S, gather, frames, cfg_name, max_s
         dist.destroy_process_group()
 
 
-def _run_tiles(tmp_path, world, W, H, B, S, gather, frames=1, cfg_name="C2", max_steps=0):
+def _run_tiles(tmp_path, world, W, H, B, S, gather, frames=1, cfg_name="C2", max_steps=0,
+               slots=2):
     out = str(tmp_path / "frame.npz")
     mp.spawn(_tiles_worker, args=(world, _free_port(), W, H, B, S, gather, frames, cfg_name,
-                                  max_steps, out), nprocs=world, join=True)
+                                  max_steps, out, slots), nprocs=world, join=True)
     with np.load(out) as z:
         return {k: z[k] for k in z.files}
 
@@ -87,13 +88,15 @@ def _c2_frame(oracle, W, H):
     return oracle.render_frame(bh, dk, cfg, configs.camera("B"), W, H, c.method, c.flags)
 
 
-@pytest.mark.parametrize("world,W,H,B,gather,frames", [
-    (2, 24, 32, 4, "all", 1), (3, 16, 24, 4, "all", 3), (2, 20, 16, 8, "image", 2),
-    (3, 16, 26, 4, "image", 4), (2, 16, 20, 8, "all", 3)])
-def test_gloo_tiles_reassemble_frame(tmp_path, oracle, world, W, H, B, gather, frames):
+@pytest.mark.parametrize("world,W,H,B,gather,frames,slots", [
+    (2, 24, 32, 4, "all", 1, 2), (3, 16, 24, 4, "all", 3, 2), (2, 20, 16, 8, "image", 2, 2),
+    (3, 16, 26, 4, "image", 4, 2), (2, 16, 20, 8, "all", 3, 2),
+    (2, 16, 20, 8, "all", 7, 4), (3, 16, 24, 4, "image", 6, 4)])  # four frames in flight
+def test_gloo_tiles_reassemble_frame(tmp_path, oracle, world, W, H, B, gather, frames, slots):
     """Every shard rendered (S = world), padded shards included (H = 26, 20): the image on
-    rank 0 is the single-process frame, several frames in flight."""
-    got = _run_tiles(tmp_path, world, W, H, B, world, gather, frames)
+    rank 0 is the single-process frame, several frames in flight (two or four buffer slots,
+    bench.py --streams auto)."""
+    got = _run_tiles(tmp_path, world, W, H, B, world, gather, frames, slots=slots)
     want = _c2_frame(oracle, W, H)
     fields = abi.SOA_FIELDS if gather == "all" else RGB_FIELDS
     assert sorted(k[4:] for k in got if k.startswith("img_")) == sorted(fields)
