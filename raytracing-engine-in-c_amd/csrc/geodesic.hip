@@ -846,11 +846,12 @@ __device__ __forceinline__ void ray_init_shared(Ray_& R, const bhrt_camera_k& cm
 // quotient, in a rare branch, otherwise (NaN den included). A t < 0 by signs (|num| > 0) is
 // negative here too, so the reference's rejection order is kept without a sign test.
 __device__ __forceinline__ bool disk_hit(const Ray_& R, double nx, double ny, double nz,
-                                         const Scene& sc, double& qx, double& qy, double& qz) {
+                                         const Scene& sc, double big, double& qx, double& qy,
+                                         double& qz) {
     const double den = (R.dx * nx + R.dy * ny) + R.dz * nz;
     const double num = -((R.px * nx + R.py * ny) + R.pz * nz);
     double t = div_nr(num, den, rcp_nr(den));
-    if (__builtin_expect(!(fabs(den) < 1.0e150), 0)) t = num / den;
+    if (__builtin_expect(!(fabs(den) < big), 0)) t = num / den;  // big = 1e150
     qx = R.px + R.dx * t;
     qy = R.py + R.dy * t;
     qz = R.pz + R.dz * t;
@@ -862,6 +863,8 @@ enum Term : int { T_NONE = 0, T_HORIZON, T_DISK, T_MAXDIST, T_MAXSTEPS };
 
 struct HSel {  // the four step sizes of the schedule, hoisted out of the kernel argument block
     double far_, r15, r5, r2_5;
+    double big;  // 1e150, the disk test's quotient bound: an SGPR pair set once, outside the
+                 // loop (as a literal it was rematerialised by two s_mov in every iteration)
 };
 
 // x unchanged, but opaque to the optimiser: the four step sizes stay four register values
@@ -880,7 +883,8 @@ __device__ __forceinline__ double opaque(double x) {
 // instead of a v_mov from the SGPR and a v_cndmask): where the loop has registers to spare
 template <bool V = false>
 __device__ __forceinline__ HSel hsel_of(const Scene& sc) {
-    return HSel{opaque<V>(sc.h_far), opaque<V>(sc.h_15), opaque<V>(sc.h_5), opaque<V>(sc.h_2_5)};
+    return HSel{opaque<V>(sc.h_far), opaque<V>(sc.h_15), opaque<V>(sc.h_5), opaque<V>(sc.h_2_5),
+                opaque<false>(1.0e150)};
 }
 
 // :543-548, state NaN/Inf recovery at the top of an iteration. One test of the sum
@@ -1028,7 +1032,7 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
         term = (R.y[1] <= sc.rs_x1_05) ? T_HORIZON : term;
         // segment k = (p_k, p_{k-1}) is stored and scanned by trace_ray iff k < max_steps
         double qx, qy, qz;
-        if (disk_hit(R, ox, oy, oz, sc, qx, qy, qz) & (R.k < sc.max_steps)) {
+        if (disk_hit(R, ox, oy, oz, sc, hs.big, qx, qy, qz) & (R.k < sc.max_steps)) {
             // the ray ends here: the hit point replaces the current point, so no extra
             // loop-carried registers hold it (store_hit reads it from R.px..pz; +0.9% on C2)
             R.px = qx;
@@ -1041,7 +1045,7 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
             // Fixed point: every later iteration repeats this one with p_j = p_{j-1} = p_k.
             // Only the duplicate segment (p_k, p_k) is new, and only if p_k != p_{k-1}.
             if (R.k + 1 < sc.max_steps && (x != ox || y != oy || z != oz) &&
-                disk_hit(R, x, y, z, sc, qx, qy, qz)) {
+                disk_hit(R, x, y, z, sc, hs.big, qx, qy, qz)) {
                 R.px = qx;
                 R.py = qy;
                 R.pz = qz;
