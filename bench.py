@@ -133,6 +133,11 @@ def parse():
                         "of the current frame frees; auto (default): 2, or 4 when calibration "
                         "frames after the warm-up take under AUTO_SHORT_MS or the frame has "
                         "fewer rays than AUTO_FILL_RAYS")
+    p.add_argument("--claim-order", choices=("default", "prev-tiles"), default="default",
+                   help="prev-tiles (opt-in): camera frames claim their 64-ray tiles longest "
+                        "first by the previous frame's steps (bhrt_set_claim_order; a renderer's "
+                        "temporal-coherence order -- optimistic here, where every frame is the "
+                        "same image)")
     p.add_argument("--weak-mode", choices=("tiles", "samples"), default="tiles",
                    help="weak configs at N GPUs: tiles = N shards of a frame (default); "
                         "samples = N sub-pixel sample planes of the configuration frame "
@@ -300,6 +305,14 @@ def main():
                 step()
             pipe.finish()
         warmup += 4 + (4 if active[0] == 4 else 0)
+    order_keep = None
+    if args.claim_order == "prev-tiles" and not samples:
+        order_keep = prev_tiles_order(pipe, frame_no[0] - 1, H, W, B, S, shard)
+        if order_keep is not None:
+            for _ in range(len(streams)):  # untimed frames in the new order
+                step()
+            pipe.finish()
+            warmup += len(streams)
     torch.cuda.synchronize()
     lib.stats(reset=True)
     if world > 1:
@@ -330,6 +343,8 @@ def main():
         dist.destroy_process_group()
         return
 
+    if order_keep is not None:
+        lib.set_claim_order(None, 0)
     rays_all = float(rays_frame) * args.steps
     mrays = rays_all / elapsed / 1e6
     launches = max(st["launches"], 1)
@@ -394,6 +409,7 @@ def main():
                          "averaged"),
             "event_avg_ms": round(kern_ms, 4),
             "streams": active[0],
+            "claim_order": args.claim_order if order_keep is not None else "default",
             "streams_policy": (f"auto: calibration frame {calib_ms:.3f} ms (4 streams under "
                                f"{AUTO_SHORT_MS} ms or under {AUTO_FILL_RAYS} rays per GPU)"
                                if auto else "fixed (--streams)"),
@@ -426,6 +442,31 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def prev_tiles_order(pipe, last, H, W, B, S, shard):
+    """The claim order (device int32 permutation of the shard's rays) that visits the 64-ray
+    tiles of the kernel's own tiling (8x8, else 16x4, else 32x2: bhrt_api.c claim_tiles) in
+    decreasing order of their longest ray's steps in frame `last`, each tile's rays in the
+    kernel's in-tile order; installed with bhrt_set_claim_order. None if no tiling fits."""
+    nrows = shard_row_count(H, B, shard, S)
+    shape = next(((tw, th) for tw, th in ((8, 8), (16, 4), (32, 2))
+                  if W % tw == 0 and nrows % th == 0), None)
+    if shape is None:
+        return None
+    tw, th = shape
+    fb = pipe.bufs[last % pipe.nslots]
+    steps = fb.views["steps"].view(-1, W)[:nrows]
+    cost = steps.view(nrows // th, th, W // tw, tw).amax(dim=(1, 3)).flatten()
+    order = torch.argsort(-cost.to(torch.int64), stable=True)
+    tc = W // tw
+    base = (order // tc) * (th * W) + (order % tc) * tw
+    w = torch.arange(64, device=steps.device)
+    offs = (w // tw) * W + (w % tw)
+    perm = (base[:, None] + offs[None, :]).flatten().to(torch.int32).contiguous()
+    torch.cuda.synchronize()
+    lib.set_claim_order(perm.data_ptr(), nrows * W)
+    return perm
 
 
 def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
