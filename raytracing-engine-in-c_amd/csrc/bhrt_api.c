@@ -666,6 +666,7 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
     kp->ctl = c->d_ctl + (size_t)slot * BHRT_SLOT_WORDS;
     kp->qhead = kp->ctl + BHRT_QHEAD_OFF;
+    kp->diag_slot = slot;
     /* (a fill kernel; a copy of pinned zeros measured the same -- small copies are blit
      * kernels too -- profiles/r04/session_h_batch) */
     HIP_TRY(hipMemsetAsync(kp->ctl, 0,
@@ -1152,7 +1153,19 @@ int bhrt_render_frame_gather(const BlackHoleParams* bh, const AccretionDiskParam
             rc_all = -1;
             break;
         }
-        if (ensure(&c->d_gather, &c->cap_gather, bytes ? bytes : 256, 0) || lazy_event(&c->g_done) ||
+        /* ... and before the buffers are freed to grow: those copies run on the ROOT's stream,
+         * and hipFree drains only this device's queues (the stream wait above orders later GPU
+         * work, not a host-side free) */
+        const size_t need = bytes ? bytes : 256;
+        if (c->g_wait_pending && c->cap_gather < need) {
+            if (hipEventSynchronize(c->g_wait) != hipSuccess) {
+                set_err("hipEventSynchronize failed");
+                rc_all = -1;
+                break;
+            }
+            c->g_wait_pending = 0;
+        }
+        if (ensure(&c->d_gather, &c->cap_gather, need, 0) || lazy_event(&c->g_done) ||
             lazy_event(&c->g_copied)) {
             rc_all = -1;
             break;

@@ -121,6 +121,8 @@ typedef struct {
                              (the AoS rays' direction field, stride 6, or packed, stride 3,
                              with rays NULL) */
     int dir_stride;
+    int diag_slot;        /* the launch's control-block slot (the BHRT_WAVE_STAMPS diagnostic
+                             build records per-wave stamps under it; unused otherwise) */
 } bhrt_kparams;
 
 /* update_particles (particle_sim.c:505-566) constants, from the BlackHoleParams and

@@ -1411,6 +1411,18 @@ __device__ __forceinline__ unsigned queue_size(unsigned ntotal, unsigned qbits, 
 #define BHRT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, 256), \
                                          amdgpu_waves_per_eu(trace_waves<METHOD, DISK, SPIN0>() > 0 ? trace_waves<METHOD, DISK, SPIN0>() : 1)))
 
+// Diagnostic build only (make DEFS=-DBHRT_WAVE_STAMPS=1, tools/wave_stamps.py): every wave of a
+// hot k_trace launch records, under the launch's control-block slot, its start and end on the
+// constant 100 MHz clock, its CU, and its trips, refills, lane-iterations and rays. The shipped
+// build has none of it.
+#ifndef BHRT_WAVE_STAMPS
+#define BHRT_WAVE_STAMPS 0
+#endif
+#if BHRT_WAVE_STAMPS
+constexpr int kStampSlots = 64, kStampWaves = 8192, kStampWords = 6;
+__device__ unsigned long long g_stamps[kStampSlots * kStampWaves * kStampWords];
+#endif
+
 // Loop iterations per trip of the persistent loop (the HUGE redo pass keeps one): RK4 6,
 // RKF45 2, from same-box sweeps of 1..8 (profiles/r02_ab_unroll.txt).
 template <int METHOD, bool SPIN0, bool HUGE>
@@ -1441,6 +1453,10 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const double as1 = kp.cam.s_r0, ac1 = kp.cam.c_r0, as2 = kp.cam.st, ac2 = kp.cam.ct,
                  as3 = kp.cam.sp, ac3 = kp.cam.cp;
     const int lane = threadIdx.x & 63;
+#if BHRT_WAVE_STAMPS
+    const unsigned long long st_t0 = (unsigned long long)wall_clock64();
+    unsigned st_trips = 0, st_refills = 0;
+#endif
     const unsigned long long below = (1ull << lane) - 1ull;
     Counters n;
     Ray_ R;
@@ -1485,6 +1501,9 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         const unsigned long long live_mask = __ballot(live);
         int n_live = __popcll(live_mask);
         if (!exhausted && (64 - n_live >= kp.refill || n_live == 0)) {
+#if BHRT_WAVE_STAMPS
+            st_refills++;
+#endif
             bool ok;
             unsigned long long id;
             if constexpr (MULTIQ) {
@@ -1606,6 +1625,9 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             if (exhausted) break;
             continue;
         }
+#if BHRT_WAVE_STAMPS
+        st_trips++;
+#endif
         if (live) {
             int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, hsel);
             // further iterations in the same trip for rays that go on: the loop's hand-over
@@ -1653,6 +1675,21 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         s2 = SPIN0 ? st : 0ull;
         s4 = SPIN0 ? 0ull : st;
     }
+#if BHRT_WAVE_STAMPS
+    if (!HUGE && lane == 0 && kp.diag_slot >= 0 && kp.diag_slot < kStampSlots) {
+        const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        if (w < (unsigned)kStampWaves) {
+            unsigned long long* p =
+                g_stamps + ((size_t)kp.diag_slot * kStampWaves + w) * kStampWords;
+            p[0] = st_t0;
+            p[1] = (unsigned long long)wall_clock64();
+            p[2] = (unsigned long long)__smid();
+            p[3] = (unsigned long long)st_trips | ((unsigned long long)st_refills << 32);
+            p[4] = s1;
+            p[5] = s0;
+        }
+    }
+#endif
     if (lane == 0) {
         if (s0) atomicAdd(kp.ctl + 1, s0);
         if (s1) atomicAdd(kp.ctl + 2, s1);
@@ -1955,3 +1992,20 @@ extern "C" int bhrt_launch_path(const bhrt_kparams* kp, const double* o4, const 
     }
     return (int)hipGetLastError();
 }
+
+#if BHRT_WAVE_STAMPS
+// Diagnostic build: copy the per-wave stamps to host memory dst (kStampSlots x kStampWaves x
+// kStampWords u64; NULL = do not copy) and, with reset, zero them. Synchronises the device.
+extern "C" __attribute__((visibility("default"))) long bhrt_diag_stamps(void* dst, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), sizeof g_stamps) != hipSuccess)
+        return -1;
+    if (reset) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps)) != hipSuccess ||
+            hipMemset(p, 0, sizeof g_stamps) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            return -1;
+    }
+    return (long)sizeof g_stamps;
+}
+#endif

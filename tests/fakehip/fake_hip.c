@@ -23,7 +23,17 @@ struct ihipEvent_t {
     int dev;
     double t;
     int recorded;
+    hipStream_t stream;      /* where it was last recorded */
+    unsigned long seq;       /* the operation count then   */
 };
+
+/* Every stream operation runs at enqueue time, but libbhrt must not rely on that: a
+ * device-to-device copy whose source is another device's memory (an xGMI peer read queued on
+ * the root's stream) counts as still reading that source until the host has waited for the
+ * copy's stream (hipStreamSynchronize, or hipEventSynchronize of an event recorded after the
+ * copy). hipFree of such a source aborts: on real HIP, hipFree drains only the owning device's
+ * queues, not the peer's that reads it (bhrt_render_frame_gather). */
+static unsigned long g_seq;
 
 static int n_devices(void) {
     const char* e = getenv("FAKEHIP_DEVICES");
@@ -46,6 +56,8 @@ typedef struct {
     uintptr_t base;
     size_t size;
     int dev;
+    hipStream_t pend_stream; /* a peer copy on this stream may still read it ... */
+    unsigned long pend_seq;  /* ... the copy's operation count (0: no pending read) */
 } alloc_t;
 static alloc_t g_alloc[4096];
 static int g_nalloc;
@@ -53,7 +65,7 @@ static int g_nalloc;
 static void track(void* p, size_t n, int dev) {
     pthread_mutex_lock(&g_mu);
     if (g_nalloc == (int)(sizeof g_alloc / sizeof *g_alloc)) FAIL("allocation table full");
-    g_alloc[g_nalloc++] = (alloc_t){(uintptr_t)p, n, dev};
+    g_alloc[g_nalloc++] = (alloc_t){(uintptr_t)p, n, dev, NULL, 0};
     pthread_mutex_unlock(&g_mu);
 }
 static int untrack(void* p, int dev) {
@@ -80,6 +92,33 @@ static int kind_of(const void* p, size_t n) {
     pthread_mutex_unlock(&g_mu);
     return k;
 }
+/* a peer read of [p, p + n) queued on stream s */
+static void mark_peer_read(const void* p, size_t n, hipStream_t s) {
+    pthread_mutex_lock(&g_mu);
+    const unsigned long q = ++g_seq;
+    for (int i = 0; i < g_nalloc; i++)
+        if ((uintptr_t)p >= g_alloc[i].base && (uintptr_t)p + n <= g_alloc[i].base + g_alloc[i].size) {
+            g_alloc[i].pend_stream = s;
+            g_alloc[i].pend_seq = q;
+        }
+    pthread_mutex_unlock(&g_mu);
+}
+/* the host waited for stream s up to operation count `upto` */
+static void host_waited(hipStream_t s, unsigned long upto) {
+    pthread_mutex_lock(&g_mu);
+    for (int i = 0; i < g_nalloc; i++)
+        if (g_alloc[i].pend_seq && g_alloc[i].pend_stream == s && g_alloc[i].pend_seq <= upto)
+            g_alloc[i].pend_seq = 0;
+    pthread_mutex_unlock(&g_mu);
+}
+static int peer_read_pending(const void* p) {
+    int hit = 0;
+    pthread_mutex_lock(&g_mu);
+    for (int i = 0; i < g_nalloc; i++)
+        if (g_alloc[i].base == (uintptr_t)p && g_alloc[i].pend_seq) hit = 1;
+    pthread_mutex_unlock(&g_mu);
+    return hit;
+}
 static int overlaps_registration(uintptr_t a, size_t n) {
     int hit = 0;
     pthread_mutex_lock(&g_mu);
@@ -99,7 +138,7 @@ static int g_nhost;
 void fakehip_declare_host(const void* p, size_t n) {
     pthread_mutex_lock(&g_mu);
     if (g_nhost == (int)(sizeof g_host / sizeof *g_host)) FAIL("host array table full");
-    g_host[g_nhost++] = (alloc_t){(uintptr_t)p, n, -4};
+    g_host[g_nhost++] = (alloc_t){(uintptr_t)p, n, -4, NULL, 0};
     pthread_mutex_unlock(&g_mu);
 }
 void fakehip_forget_host(const void* p) {
@@ -161,6 +200,8 @@ hipError_t hipMalloc(void** p, size_t n) {
 }
 hipError_t hipFree(void* p) {
     if (!p) return hipSuccess;
+    if (peer_read_pending(p))
+        FAIL("hipFree of %p while a peer copy queued on another device's stream may still read it", p);
     if (!untrack(p, g_dev)) FAIL("hipFree of %p: not a device-%d allocation", p, g_dev);
     free(p);
     return hipSuccess;
@@ -224,6 +265,7 @@ hipError_t hipExtStreamCreateWithCUMask(hipStream_t* s, uint32_t n, const uint32
 }
 hipError_t hipStreamSynchronize(hipStream_t s) {
     check_stream(s);
+    host_waited(s, (unsigned long)-1);
     return hipSuccess;
 }
 hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned flags) {
@@ -247,6 +289,10 @@ hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
     check_stream(s);
     if (e->dev != g_dev) FAIL("event of device %d recorded on device %d", e->dev, g_dev);
     e->recorded = 1;
+    pthread_mutex_lock(&g_mu);
+    e->stream = s;
+    e->seq = ++g_seq;
+    pthread_mutex_unlock(&g_mu);
     return hipSuccess;
 }
 
@@ -265,7 +311,7 @@ hipError_t hipDeviceEnablePeerAccess(int peer, unsigned flags) {
     return hipSuccess;
 }
 hipError_t hipEventSynchronize(hipEvent_t e) {
-    (void)e;
+    if (e->recorded) host_waited(e->stream, e->seq);
     return hipSuccess;
 }
 hipError_t hipEventElapsedTime(float* ms, hipEvent_t a, hipEvent_t b) {
@@ -301,6 +347,7 @@ hipError_t hipMemcpy(void* dst, const void* src, size_t n, hipMemcpyKind kind) {
 hipError_t hipMemcpyAsync(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t s) {
     check_stream(s);
     check_copy(dst, src, n, kind, kind == hipMemcpyDeviceToHost);
+    if (kind == hipMemcpyDeviceToDevice && kind_of(src, n) != g_dev) mark_peer_read(src, n, s);
     memcpy(dst, src, n);
     return hipSuccess;
 }
@@ -312,6 +359,8 @@ hipError_t hipMemcpy2DAsync(void* dst, size_t dpitch, const void* src, size_t sp
         check_copy((char*)dst + r * dpitch, (const char*)src + r * spitch, width, kind,
                    kind == hipMemcpyDeviceToHost);
         memcpy((char*)dst + r * dpitch, (const char*)src + r * spitch, width);
+        if (kind == hipMemcpyDeviceToDevice && kind_of((const char*)src + r * spitch, width) != g_dev)
+            mark_peer_read((const char*)src + r * spitch, width, s);
     }
     return hipSuccess;
 }
@@ -320,6 +369,7 @@ hipError_t hipMemcpyPeerAsync(void* dst, int dst_dev, const void* src, int src_d
     check_stream(s);
     if (kind_of(dst, n) != dst_dev || kind_of(src, n) != src_dev)
         FAIL("peer copy %p (device %d) <- %p (device %d): wrong devices", dst, dst_dev, src, src_dev);
+    if (src_dev != g_dev) mark_peer_read(src, n, s);
     memcpy(dst, src, n);
     return hipSuccess;
 }
