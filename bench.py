@@ -86,7 +86,12 @@ if __name__ == "__main__":
 # and work on one queue runs in order: with the torch default stream, the two render streams and
 # RCCL's stream of an N-GPU run, a shared queue would put a frame's gather behind the next
 # frame's trace kernel. 8 gives each of them a queue of its own.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+# The effective value is recorded in the JSON line ("runtime"); BHRT_BENCH_HW_QUEUES=default
+# keeps the runtime's own setting (the stock 4 on the box), for the rate a default-configured
+# renderer process gets.
+HWQ_ASKED = os.environ.get("GPU_MAX_HW_QUEUES")
+if (os.environ.get("BHRT_BENCH_HW_QUEUES") != "default" and
+        int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8):
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
@@ -212,6 +217,9 @@ def main():
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     if world > 1:
+        # RCCL times each collective on its own stream (Work.get_duration): the gather's GPU
+        # time per frame goes into the JSON line ("dist")
+        os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
         if shared:
             dist.init_process_group("gloo")
         else:
@@ -315,6 +323,7 @@ def main():
             warmup += len(streams)
     torch.cuda.synchronize()
     lib.stats(reset=True)
+    pipe.collective_ms.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -327,6 +336,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_rank = elapsed
     st = lib.stats(reset=True)
     if world > 1:
         red = "cpu" if shared else device  # (gloo reduces host tensors)
@@ -336,8 +346,18 @@ def main():
         tot = torch.tensor([st["iterations"]], dtype=torch.float64, device=red)
         dist.all_reduce(tot)
         iterations_all = tot.item()
+        # per rank: trace-kernel GPU time per frame, its own wall time, the gather's GPU time
+        nl = max(st["launches"], 1)
+        cms = pipe.collective_ms
+        mine = torch.tensor([st["span_ms"] / nl, st["kernel_ms"] / nl, elapsed_rank,
+                             sum(cms) / len(cms) if cms else float("nan"), len(cms)],
+                            dtype=torch.float64, device=red)
+        per_rank = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
+        per_rank = torch.stack(per_rank).cpu().numpy()
     else:
         iterations_all = st["iterations"]
+        per_rank = None
 
     if rank != 0:
         dist.destroy_process_group()
@@ -434,6 +454,35 @@ def main():
             issued_fp64_frac=round(issued / FP64_PEAK_TFLOPS, 5),
             valu_issue_busy=prof.get("valu_issue_busy"),
             pmc=f"profiles/pmc_{args.config}.json")
+    out["runtime"] = {
+        "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"),
+        "hw_queues_set_by_bench": os.environ.get("GPU_MAX_HW_QUEUES") != HWQ_ASKED,
+        "note": "bench.py raises HIP's hardware queues per process to 8 unless "
+                "BHRT_BENCH_HW_QUEUES=default (the box's stock value is 4): with the render "
+                "streams, torch's default stream and RCCL's, 4 queues would put a frame's "
+                "collective behind the next frame's trace kernel"}
+    if per_rank is not None:
+        cms = per_rank[:, 3]
+        out["dist"] = {
+            "world_size": dist.get_world_size(),
+            "backend": dist.get_backend(),
+            "rccl_version": (".".join(str(v) for v in torch.cuda.nccl.version())
+                             if dist.get_backend() == "nccl" else None),
+            "trace_ms_per_frame": {"max": round(float(per_rank[:, 0].max()), 4),
+                                   "mean": round(float(per_rank[:, 0].mean()), 4),
+                                   "per_rank": [round(float(v), 4) for v in per_rank[:, 0]]},
+            "rank_wall_ms_per_frame": {
+                "max": round(float(per_rank[:, 2].max()) / args.steps * 1e3, 4),
+                "min": round(float(per_rank[:, 2].min()) / args.steps * 1e3, 4)},
+            "gather_ms_per_frame": ({"max": round(float(np.nanmax(cms)), 4),
+                                     "mean": round(float(np.nanmean(cms)), 4),
+                                     "per_rank": [round(float(v), 4) for v in cms]}
+                                    if np.isfinite(cms).any() else None),
+            "gather": (f"one {dist.get_backend()} gather of the {args.gather} fields to rank 0 "
+                       "per frame, overlapped with the next frame; its GPU time from the "
+                       "process group's own events (TORCH_NCCL_ENABLE_TIMING; not measured "
+                       "with gloo)"),
+        }
     if world == 1 and not args.no_host_path and S == 1:  # (bhrt_render_frame: whole images)
         out["host_path"] = host_path_rate(c, bh, dk, cfg, cam, W, H)
     if world == 1 and not args.no_cpu_baseline:

@@ -267,6 +267,8 @@ typedef struct {
     double   span_ms;       /* per GPU: first trace-kernel start to last trace-kernel end
                                since the reset (summed over GPUs); launches overlapping on
                                several streams make this, not kernel_ms, the GPU time     */
+    uint64_t redo_launches; /* of those launches, how many were followed by the redo pass
+                               (left out where no ray can need it)   */
 } bhrt_stats;
 
 /* Number of rows of an image of `height` rows owned by shard rows->shard. */

@@ -172,6 +172,9 @@ class FramePipeline:
         if mode == "samples" and world > 1 and not set(self.gather) <= set(RGB_FIELDS):
             raise ValueError("samples mode reduces the colour planes only")
         self.works = [None] * self.nslots
+        # the collective's own GPU time per completed frame (ms), where the process group
+        # times its work (RCCL with TORCH_NCCL_ENABLE_TIMING=1: Work.get_duration)
+        self.collective_ms = []
         self.frames = 0
         self.last = None
         self.images = self.gathered = self.colour = None
@@ -243,6 +246,10 @@ class FramePipeline:
             return
         if w is not True:
             w.wait()
+            try:
+                self.collective_ms.append(float(w.get_duration()))
+            except Exception:  # (gloo, or timing not enabled: not measured)
+                pass
             if self.staged and self.rank == 0:
                 self.gathered[slot].copy_(self.host_recv[slot])
         self.works[slot] = None

@@ -105,6 +105,7 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 
 typedef struct {
     int slot;
+    int redo; /* the redo pass was launched after the hot one */
     hipEvent_t ev0, ev1;
 } pending_t;
 
@@ -444,6 +445,7 @@ static int harvest(devctx_t* c) {
         g_stats.stages_far += w[4];
         g_stats.stages_kerr += w[5];
         g_stats.rays_redone += w[6];
+        g_stats.redo_launches += (uint64_t)c->pend[i].redo;
         g_stats.launches += 1;
         g_stats.kernel_ms += ms;
     }
@@ -513,6 +515,61 @@ static int far_bounded(const bhrt_scene_k* s) {
     const double logv = log2(0x1p40 + N * 20.0 * h * W) + N * log1p(2.0 * h * W * C) / log(2.0);
     const double logp = log2(0x1p40 + N * 2.0 * h * W * (exp2(fmin(logv, 1000.0)) + 10.0 * h * S));
     return logv <= 400.0 && logp <= 400.0;
+}
+
+/* Whether no ray that starts at this origin can be handed to the redo pass (geodesic.hip k_trace:
+ * a finite sincos argument |x| >= 2^20, a far-field state the host could not prove bounded, or
+ * -- on the zero-acceleration Kerr paths -- |state[5]| >= rot_vmax). Then the redo launch is
+ * left out (launch_trace_pair): one dispatch less per frame, and a frame's completion no longer
+ * waits behind the next frame's persistent workgroups for a wave slot.
+ * The live state is (t, r, theta, phi, tdot, rdot); ray_derivatives reads it shifted, so the
+ * derivatives of components 0..2 are components 3..5 ("velocities" V) and those of 3..5 are
+ * accelerations: clamped to 10, zero (Kerr), or -- far-field branch, only where y0 > 15 rs --
+ * y5 * 2M / y0^2 with a factor below C = 2M / (15 rs)^2. With h the largest step size, S the
+ * largest stage weight sum (RK4 1, RKF45 17.4 -> 18) and W the final combination's (RK4 1,
+ * RKF45 1.4 -> 1.5): without the far-field branch a stage velocity is at most V + 10 h S, a step
+ * moves V by at most 10 h W and the positions P by at most h W (V + 10 h S); with it (q = h S C
+ * < 1/2) a stage velocity is at most 2 (V + 10 h S), V' <= g V + 20 h W with g = 1 + 2 h W C,
+ * and P moves by at most 2 h W (V + 10 h S) (far_bounded's argument). The initial state: t = 0,
+ * r, theta, phi of the origin, rdot = n.e_r <= 1 and tdot^2 <= (|g_rr| + (g_hh / r^2)(1 + 1 /
+ * sin^2 theta)) / |g_tt| (n a unit vector; its components on the orthonormal e_theta, e_phi
+ * give theta-dot = n.e_theta / r, phi-dot = n.e_phi / (r sin theta)). Every sincos argument
+ * of the loop is a (stage) value of components 1..3, so a bound below 2^20 proves the claim. */
+static int origin_no_evict(const bhrt_scene_k* s, double r, double th, double ph, double st,
+                           int st_tiny, double g_tt, double g_rr, double g_hh, int far) {
+    if (s->max_steps <= 0) return 1;
+    const int rkf = s->method == INTEGRATOR_RKF45;
+    if (!rkf && s->method != INTEGRATOR_RK4) return 1; /* (no-op integrators: no step at all) */
+    if (!s->spin0 && !far) /* the rotation paths: no sincos in the loop; |rdot| <= 1 + 2^-50 */
+        return s->rot_vmax > 1.001;
+    if (far && !s->far_bounded) return 0;
+    if (!(isfinite(r) && isfinite(th) && isfinite(ph) && isfinite(g_tt) && isfinite(g_rr) &&
+          isfinite(g_hh) && g_tt != 0.0 && r != 0.0))
+        return 0;
+    const double h = fmax(fmax(fabs(s->h_2_5), fabs(s->h_5)), fmax(fabs(s->h_15), fabs(s->h_far)));
+    if (!isfinite(h)) return 0;
+    const double S = rkf ? 18.0 : 1.0, W = rkf ? 1.5 : 1.0, N = (double)s->max_steps;
+    const double sl = 1.0 + 1e-6; /* slack for the rounding of the set-up's products */
+    const double inv_st2 = st_tiny ? 0.0 : 1.0 / (st * st);
+    if (!isfinite(inv_st2)) return 0;
+    const double vt2 = (fabs(g_rr) + fabs(g_hh) / (r * r) * (1.0 + inv_st2)) / fabs(g_tt);
+    const double V0 = fmax(fmax(fabs(ph), sqrt(vt2) * sl), sl);
+    const double P0 = fmax(fabs(r), fabs(th));
+    double V, P, B;
+    if (!far || s->two_m == 0.0) {
+        V = V0 + N * 10.0 * h * W;
+        P = P0 + N * h * W * (V + 10.0 * h * S);
+        B = fmax(P + h * S * (V + 10.0 * h * S), V + 10.0 * h * S);
+    } else {
+        const double C = s->two_m / (s->rs_x15 * s->rs_x15) * (1.0 + 1e-9);
+        if (!isfinite(C) || !(h * S * C < 0.5)) return 0;
+        const double lg = N * log1p(2.0 * h * W * C);
+        if (!(lg < 40.0)) return 0;
+        V = exp(lg) * (V0 + N * 20.0 * h * W);
+        P = P0 + N * 2.0 * h * W * (V + 10.0 * h * S);
+        B = fmax(P + 2.0 * h * S * (V + 10.0 * h * S), 2.0 * (V + 10.0 * h * S));
+    }
+    return isfinite(B) && B * sl < 1048576.0;
 }
 
 static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const AccretionDiskParams* dk,
@@ -650,6 +707,8 @@ static void fill_origin(bhrt_kparams* kp, const Vector3D* origin) {
     k->sp = sp;
     k->s_r0 = sin(r);
     k->c_r0 = cos(r);
+    kp->no_evict = origin_no_evict(&kp->sc, r, th, ph, st, k->st_tiny, m.g_tt, m.g_rr, m.g_thth,
+                                   k->use_approx);
 }
 
 /* one timed trace-kernel launch on `stream` (the context's own if NULL) */
@@ -681,6 +740,7 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     }
     pending_t* p = &c->pend[c->npend];
     p->slot = slot;
+    p->redo = !(kp->skip_redo && kp->no_evict);
     p->ev0 = c->evpool[2 * c->npend];
     p->ev1 = c->evpool[2 * c->npend + 1];
     int e = bhrt_launch_trace(kp, (void*)stream, (void*)p->ev0, (void*)p->ev1);

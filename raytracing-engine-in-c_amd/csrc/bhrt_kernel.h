@@ -113,6 +113,9 @@ typedef struct {
                              permutation of [0, n)); NULL = ray id order */
     int skip_redo;        /* the redo launch may be left out where no ray can be evicted
                              (geodesic.hip launch_trace_pair); BHRT_SKIP_REDO=0: always launch */
+    int no_evict;         /* the host proved that no ray of this launch can be handed to the
+                             redo pass (bhrt_api.c origin_no_evict; camera frames and ray
+                             arrays with one shared origin) */
     int block_lanes;      /* lanes per workgroup of the hot trace launch (64, 128 or 256) */
     int rays_shared;      /* BHRT_SRC_RAYS whose every origin is cam.pos (the host checked):
                              cam's origin block is filled as for a camera frame, and the

@@ -291,6 +291,14 @@ __device__ __forceinline__ void repair_clamp(double (&d)[6]) {
 // every other stage takes the instantiation's one other branch, and k_trace derives that count
 // from the iterations (the HUGE redo, whose RKF45 attempts can stop after stage 1, counts
 // every stage).
+// Stage-counting build (make DEFS=-DBHRT_COUNT_STAGES=1 -> diag/libbhrt_count.so, built by
+// __graft_entry__.build()): every instantiation counts each stage's branch one by one, as the
+// FAR && HUGE redo pass always does, instead of deriving the split from the iterations -- the
+// GPU test test_stage_counts_are_counted checks that both give the same counters (the FLOP
+// credit of bench.py rests on the derived ones) and the same frame.
+#ifndef BHRT_COUNT_STAGES
+#define BHRT_COUNT_STAGES 0
+#endif
 template <bool SPIN0, bool FAR, bool HUGE>
 __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const Scene& sc,
                                     bool far_ok, Counters& n, Trig1& tr, bool first) {
@@ -312,7 +320,7 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
         } else {
             shift_or_eval(tr.a, tr.s, tr.c, y[1], st, ct, HUGE ? nullptr : &n);
         }
-        if (FAR && HUGE) n.full++;
+        if ((FAR && HUGE) || BHRT_COUNT_STAGES) n.full++;
         // Fast form, straight-line: the same three accelerations with the divisions as one
         // reciprocal and the products regrouped -- d3 = -M/r^2 + r (v_th^2 + (sin th v_ph)^2),
         // d4 = -2 v_r v_th / r + (sin th v_ph)(cos th v_ph),
@@ -349,7 +357,7 @@ __device__ __forceinline__ void rhs(const double (&y)[6], double (&d)[6], const 
     d[3] = 0.0;
     d[4] = 0.0;
     d[5] = 0.0;
-    if (FAR && HUGE) n.kerr++;
+    if ((FAR && HUGE) || BHRT_COUNT_STAGES) n.kerr++;
     // Far-field and Kerr stages: the repair / clamps never change a value here but run as the
     // reference's pass whenever a component is not a plain |d| <= 10 value (NaN and Inf fail
     // the test). d[0..2] = y[3..5] need no test: the iteration starts from a finite state, and
@@ -1522,7 +1530,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                     const unsigned want = need - avail;
                     unsigned b = 0, e = 0;
                     bool hopped = false;
-                    for (;;) {  // wave-uniform; at most Q - 1 hops over the wave's life
+                    for (;;) {  // wave-uniform; ends once a claim lands or every queue is dry
                         const unsigned size = queue_size(ntotal, qbits, cur);
                         unsigned long long* const hp = heads + (size_t)cur * qstride;
                         unsigned c = want;
@@ -1532,20 +1540,35 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                             if (c < want) c = want;
                         }
                         unsigned long long base = 0;
-                        if (lane == 0) {
-                            // a queue reached by a hop may be dry already: look before claiming
-                            if (hopped)
-                                base = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            if (base < size) base = atomicAdd(hp, (unsigned long long)c);
-                        }
+                        if (lane == 0) base = atomicAdd(hp, (unsigned long long)c);
                         base = __shfl(base, 0);
                         if (base < size) {
                             b = (unsigned)base;
                             e = base + c < size ? (unsigned)(base + c) : size;
                             break;
                         }
-                        if (++moves >= nq) break;
-                        cur = (cur + 1u) & (nq - 1u);
+                        // Queue `cur` is dry. The queues not yet left behind are looked at in
+                        // ONE round trip -- lane k reads the head of queue cur + 1 + k -- and
+                        // the wave moves to the first with ids left (a dry queue stays dry).
+                        // Hopping one queue per round trip had cost a wave up to 15 serial
+                        // atomic round trips (~30 us) at the end of every launch: a quarter of a
+                        // strong-scaled C4 shard's wave lifetime (tools/wave_stamps.py).
+                        const unsigned left = nq - 1u - moves;
+                        bool room = false;
+                        if ((unsigned)lane < left) {
+                            const unsigned qk = (cur + 1u + (unsigned)lane) & (nq - 1u);
+                            room = __hip_atomic_load(heads + (size_t)qk * qstride, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) <
+                                   (unsigned long long)queue_size(ntotal, qbits, qk);
+                        }
+                        const unsigned long long rm = __ballot(room);
+                        if (rm == 0ull) {
+                            moves = nq;
+                            break;
+                        }
+                        const unsigned k = (unsigned)__builtin_ctzll(rm);
+                        moves += k + 1u;
+                        cur = (cur + 1u + k) & (nq - 1u);
                         hi = 0u;
                         hopped = true;
                     }
@@ -1665,7 +1688,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const unsigned long long s0 = wave_sum(n.rays), s1 = wave_sum(n.iters),
                              s3 = wave_sum(n.far_);
     unsigned long long s2, s4;
-    if (FAR && HUGE) {  // stages counted one by one
+    if ((FAR && HUGE) || BHRT_COUNT_STAGES) {  // stages counted one by one
         s2 = wave_sum(n.full);
         s4 = wave_sum(n.kerr);
     } else {  // every stage that was not a far-field one took the instantiation's branch
@@ -1856,14 +1879,13 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     bhrt_kparams k = kp;
     k.claim_shift = claim_shift(blocks, kp.claim_div, kp.queue_bits, lanes);
     k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, lanes, 0, st>>>(k);
-    // A camera launch on the zero-acceleration paths (C4, C5) evicts no ray: its loop has no
-    // sincos that can raise the large-argument flag (rotation_trig), and the one refill-time
-    // test, |state[5]| < rot_vmax, holds for every camera ray (|state[5]| = |v_r| is a dot
-    // product of two unit vectors, <= 1 + 2^-50, checked against rot_vmax here) -- so no redo
-    // launch follows, one dispatch less per frame (what a strong-scaled shard pays for)
-    if (rotation_trig<METHOD, SPIN0, FAR, false>() && kp.src == BHRT_SRC_CAMERA &&
-        kp.sc.rot_vmax > 1.001 && kp.skip_redo)
-        return;
+    // A launch the host proved eviction-free (bhrt_api.c origin_no_evict: every ray starts at
+    // one origin, and every state the loop can reach keeps its sincos arguments below 2^20 --
+    // C1, C2, C3 -- or, on the zero-acceleration paths, C4 and C5, the loop has no sincos and
+    // the one refill-time test |state[5]| < rot_vmax holds for every unit direction) hands no
+    // ray over: no redo launch follows, one dispatch less per frame, and the frame's end no
+    // longer waits behind the next frame's persistent workgroups for a wave slot
+    if (kp.no_evict && kp.skip_redo) return;
     // rays evicted by the large-argument check (normally none: every wave exits at once). 64
     // workgroups: the evicted rays are rare, and a full-chip grid of waves that only read the
     // count and exit costs ~15 us per frame (C3 +8.5% same-box, profiles/r02_ab_v24.txt)

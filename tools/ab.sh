@@ -12,7 +12,7 @@ for round in $(seq 1 ${ROUNDS:-2}); do
     name=${v%%:*}; envset=""; [ "$name" != "$v" ] && envset=${v#*:} && envset=${envset//,/ }
     if [ "$name" = base ]; then lib=raytracing-engine-in-c_amd/libbhrt.so; else lib=raytracing-engine-in-c_amd/ab/libbhrt_$name.so; fi
     tag=$(echo "$v" | tr ':=' '__')
-    env $envset BHRT_LIB=$lib timeout -k 10 300 python bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline $EXTRA > $OUT/${CFG}_${tag}_$round.json 2>$OUT/${CFG}_${tag}_$round.err || { echo "$v failed"; tail -3 $OUT/${CFG}_${tag}_$round.err; exit 1; }
+    env $envset BHRT_LIB=$lib timeout -k 10 300 python bench.py --config $CFG --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline $EXTRA > $OUT/${CFG}_${tag}_$round.json 2>$OUT/${CFG}_${tag}_$round.err || { echo "$v failed"; tail -3 $OUT/${CFG}_${tag}_$round.err; exit 1; }
     python3 -c "import json,sys; d=json.load(open('$OUT/${CFG}_${tag}_$round.json')); print('$CFG', '$v', $round, d['value'], d['kernel']['avg_ms'])"
   done
 done

@@ -16,7 +16,7 @@
 #   ab             interleaved A/B of $VARIANTS on $AB_CFGS (tools/ab.sh; $ROUNDS rounds)
 #   ab_tests       the GPU parity suite against each build in $TEST_VARIANTS
 #   stamps         per-wave stamps of $STAMP_RUNS ("CFG:PLAN:SHARD:STREAMS ...") with the
-#                  diagnostic build ab/libbhrt_stamps.so (tools/wave_stamps.py)
+#                  diagnostic build diag/libbhrt_stamps.so (tools/wave_stamps.py)
 #   steps          per-ray step maps of C2, C4, C5 (tools/dump_steps.py)
 #   cmd            run $CMD (one extra command, under a 600 s limit)
 set -o pipefail
@@ -74,7 +74,7 @@ for step in "$@"; do
     for run in ${STAMP_RUNS:-C4:8:0:4 C4:1:0:2}; do
       IFS=: read cfg plan shard streams <<< "$run"
       f=$OUT/stamps_${cfg}_p${plan}_s${shard}_x${streams}.npz
-      BHRT_LIB=raytracing-engine-in-c_amd/ab/libbhrt_stamps.so timeout -k 10 300 python tools/wave_stamps.py \
+      BHRT_LIB=raytracing-engine-in-c_amd/diag/libbhrt_stamps.so timeout -k 10 300 python tools/wave_stamps.py \
         --config $cfg --plan-gpus $plan --shard $shard --streams $streams --frames ${FRAMES:-20} --out $f \
         > $OUT/stamps.log 2>&1 || fail stamps $OUT/stamps.log
       python tools/wave_stamps.py --analyse $f

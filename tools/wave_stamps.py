@@ -1,9 +1,8 @@
 #!/usr/bin/env python3
 """Per-wave timeline of the hot trace kernel under bench.py's frame loop (diagnostic build).
 
-  make -C raytracing-engine-in-c_amd/csrc OBJ=/tmp/stb DEFS=-DBHRT_WAVE_STAMPS=1 \
-       OUT=$PWD/raytracing-engine-in-c_amd/ab/libbhrt_stamps.so
-  BHRT_LIB=raytracing-engine-in-c_amd/ab/libbhrt_stamps.so \
+  make -C raytracing-engine-in-c_amd/csrc diag     # -> diag/libbhrt_stamps.so
+  BHRT_LIB=raytracing-engine-in-c_amd/diag/libbhrt_stamps.so \
       python tools/wave_stamps.py --config C4 --plan-gpus 8 --shard 0 --streams 4 --frames 20 \
       --out gpurun_out/stamps_C4_p8.npz
   python tools/wave_stamps.py --analyse gpurun_out/stamps_C4_p8.npz
@@ -28,6 +27,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
 
 SLOTS, WAVES, WORDS = 64, 8192, 6
+# bench.py's hardware-queue setting (read when HIP initialises)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 
 def run(a):
