@@ -90,9 +90,22 @@ if __name__ == "__main__":
 # keeps the runtime's own setting (the stock 4 on the box), for the rate a default-configured
 # renderer process gets.
 HWQ_ASKED = os.environ.get("GPU_MAX_HW_QUEUES")
+
+
+def _hw_queues_wanted():
+    """8, or 16 with more than four render streams (--streams 5..8): one queue per stream"""
+    a = sys.argv[1:]
+    for i, v in enumerate(a):
+        n = v.split("=", 1)[1] if v.startswith("--streams=") else (
+            a[i + 1] if v == "--streams" and i + 1 < len(a) else None)
+        if n is not None and n.isdigit() and int(n) > 4:
+            return 16
+    return 8
+
+
 if (os.environ.get("BHRT_BENCH_HW_QUEUES") != "default" and
-        int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8):
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+        int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < _hw_queues_wanted()):
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_hw_queues_wanted())
 
 sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
 
@@ -199,8 +212,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     auto = args.streams == "auto"
-    if not auto and args.streams not in ("1", "2", "3", "4"):
-        raise SystemExit("--streams must be 1..4 or auto")
+    if not auto and args.streams not in ("1", "2", "3", "4", "5", "6", "7", "8"):
+        raise SystemExit("--streams must be 1..8 or auto")
     nstreams = 2 if auto else int(args.streams)  # FramePipeline keeps one buffer slot per stream
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")

@@ -270,6 +270,7 @@ int bhrt_device_count(void) {
     return n;
 }
 
+static hipError_t ring_zero(devctx_t* c);
 static devctx_t* ctx_get(int device) {
     if (device < 0 || device >= BHRT_MAX_DEV) {
         set_err("device %d out of range", device);
@@ -286,6 +287,11 @@ static devctx_t* ctx_get(int device) {
     if (hipMalloc((void**)&c->d_ctl,
                   (size_t)BHRT_RING * BHRT_SLOT_WORDS * sizeof(unsigned long long)) != hipSuccess) {
         set_err("cannot create HIP stream / control blocks on device %d", device);
+        free(c);
+        return NULL;
+    }
+    if (ring_zero(c) != hipSuccess) {
+        set_err("cannot zero the control blocks on device %d", device);
         free(c);
         return NULL;
     }
@@ -421,6 +427,14 @@ static void* stream_scratch(devctx_t* c, hipStream_t stream, size_t bytes) {
     return c->scratch[slot].p;
 }
 
+/* zero the whole control ring (no launch of this context may be in flight) */
+static hipError_t ring_zero(devctx_t* c) {
+    hipError_t e = hipMemsetAsync(c->d_ctl, 0,
+                                  (size_t)BHRT_RING * BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                                  (hipStream_t)0);
+    return e != hipSuccess ? e : hipStreamSynchronize((hipStream_t)0);
+}
+
 /* fold finished launches into g_stats (waits for them) */
 static int harvest(devctx_t* c) {
     if (c->npend == 0) return 0;
@@ -431,6 +445,10 @@ static int harvest(devctx_t* c) {
                         BHRT_SLOT_WORDS * sizeof(unsigned long long),
                         BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
                         hipMemcpyDeviceToHost));
+    /* every launch of the ring has completed: zero it for the next 64 (launch() itself issues
+     * no memset -- a fill kernel per frame that had to wait for a free wave slot behind the
+     * other frames' persistent kernels; a slot is reused only after it was harvested here) */
+    HIP_TRY(ring_zero(c));
     for (int i = 0; i < c->npend; i++) {
         float ms = 0.f, t0 = 0.f, t1 = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, c->pend[i].ev0, c->pend[i].ev1));
@@ -726,12 +744,12 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     kp->ctl = c->d_ctl + (size_t)slot * BHRT_SLOT_WORDS;
     kp->qhead = kp->ctl + BHRT_QHEAD_OFF;
     kp->diag_slot = slot;
-    /* (a fill kernel; a copy of pinned zeros measured the same -- small copies are blit
-     * kernels too -- profiles/r04/session_h_batch) */
-    HIP_TRY(hipMemsetAsync(kp->ctl, 0,
-                           (BHRT_QHEAD_OFF + ((size_t)kp->queue_stride << kp->queue_bits)) *
-                               sizeof(unsigned long long),
-                           stream));
+    /* (the slot was zeroed when it was last harvested, or at the context's creation) */
+    if (env_int("BHRT_LAUNCH_MEMSET", 0))  /* A/B: the per-launch fill kernel of round 4 */
+        HIP_TRY(hipMemsetAsync(kp->ctl, 0,
+                               (BHRT_QHEAD_OFF + ((size_t)kp->queue_stride << kp->queue_bits)) *
+                                   sizeof(unsigned long long),
+                               stream));
     if (!c->span_on) {
         HIP_TRY(hipEventRecord(c->span_ref, stream));
         c->span_on = 1;

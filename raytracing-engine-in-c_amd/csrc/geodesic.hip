@@ -1427,7 +1427,7 @@ __device__ __forceinline__ unsigned queue_size(unsigned ntotal, unsigned qbits, 
 #define BHRT_WAVE_STAMPS 0
 #endif
 #if BHRT_WAVE_STAMPS
-constexpr int kStampSlots = 64, kStampWaves = 8192, kStampWords = 6;
+constexpr int kStampSlots = 64, kStampWaves = 8192, kStampWords = 8;
 __device__ unsigned long long g_stamps[kStampSlots * kStampWaves * kStampWords];
 #endif
 
@@ -1463,7 +1463,8 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const int lane = threadIdx.x & 63;
 #if BHRT_WAVE_STAMPS
     const unsigned long long st_t0 = (unsigned long long)wall_clock64();
-    unsigned st_trips = 0, st_refills = 0;
+    unsigned st_trips = 0, st_refills = 0, st_claims = 0;
+    unsigned long long st_claim_t = 0, st_first = 0;  // time in claim round trips; the first's
 #endif
     const unsigned long long below = (1ull << lane) - 1ull;
     Counters n;
@@ -1540,8 +1541,18 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                             if (c < want) c = want;
                         }
                         unsigned long long base = 0;
+#if BHRT_WAVE_STAMPS
+                        const unsigned long long tq0 = (unsigned long long)wall_clock64();
+#endif
                         if (lane == 0) base = atomicAdd(hp, (unsigned long long)c);
                         base = __shfl(base, 0);
+#if BHRT_WAVE_STAMPS
+                        {
+                            const unsigned long long dtq = (unsigned long long)wall_clock64() - tq0;
+                            st_claim_t += dtq;
+                            if (st_claims++ == 0) st_first = dtq;
+                        }
+#endif
                         if (base < size) {
                             b = (unsigned)base;
                             e = base + c < size ? (unsigned)(base + c) : size;
@@ -1710,6 +1721,8 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             p[3] = (unsigned long long)st_trips | ((unsigned long long)st_refills << 32);
             p[4] = s1;
             p[5] = s0;
+            p[6] = st_claim_t | ((unsigned long long)st_claims << 48);
+            p[7] = st_first;
         }
     }
 #endif

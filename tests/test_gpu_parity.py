@@ -953,22 +953,34 @@ def test_rkf45_accept_band(bhrt_lib):
     assert near.sum() > 1000 and want[near].any() and (~want[near]).any()  # the band was hit
 
 
-# Small frames of every config, and cameras A / V (V's origin lies beyond 15 rs: the far-field
-# instantiations, whose stages take either branch per ray)
+# Small frames of every config, and cameras A / V; "FAR" is C2's scene at M = 0.5 (15 rs = 15,
+# so camera B's origin lies beyond it: the far-field instantiations, and long rays whose
+# state[0] -- read as r by ray_derivatives -- passes 15 rs, so stages take either branch)
 STAGE_CASES = [("C1", "B", 64, 48), ("C2", "B", 96, 54), ("C2", "V", 96, 54), ("C2", "A", 64, 36),
                ("C3", "B", 96, 54), ("C3", "V", 64, 36), ("C4", "B", 128, 72), ("C4", "V", 96, 54),
-               ("C5", "B", 128, 72)]
+               ("C5", "B", 128, 72), ("FAR", "B", 64, 36)]
+
+
+def _stage_scene(cname):
+    """(bh, disk, cfg, method, flags) of a STAGE_CASES entry"""
+    if cname == "FAR":
+        return (abi.black_hole(0.5, 0.0), abi.disk(3.0, 20.0, 1.0, 1.0),
+                abi.sim_config(0.1, 100.0, 1000, 1e-6), abi.INTEGRATOR_RK4, 0)
+    c = configs.CONFIGS[cname]
+    return (*c.scene(), c.method, c.flags)
+
 
 _COUNT_CHILD = r"""
 import json, sys
 sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[2])
 from bhrt import configs, lib
+from test_gpu_parity import _stage_scene
 out = []
-for cname, camname, W, H in json.loads(sys.argv[2]):
-    c = configs.CONFIGS[cname]
-    bh, dk, cfg = c.scene()
+for cname, camname, W, H in json.loads(sys.argv[3]):
+    bh, dk, cfg, method, flags = _stage_scene(cname)
     lib.stats(reset=True)
-    f = lib.render_frame(bh, dk, cfg, configs.camera(camname), W, H, c.method, c.flags)
+    f = lib.render_frame(bh, dk, cfg, configs.camera(camname), W, H, method, flags)
     st = lib.stats(reset=True)
     out.append({"stats": {k: st[k] for k in ("rays", "iterations", "stages_full", "stages_far",
                                              "stages_kerr")},
@@ -991,27 +1003,27 @@ def test_stage_counts_are_counted(bhrt_lib):
     assert os.path.exists(lib_count), "diag/libbhrt_count.so not built (__graft_entry__.build())"
     env = dict(os.environ, BHRT_LIB=lib_count)
     r = subprocess.run([sys.executable, "-c", _COUNT_CHILD,
-                        os.path.join(ROOT, "raytracing-engine-in-c_amd"), json.dumps(STAGE_CASES)],
+                        os.path.join(ROOT, "raytracing-engine-in-c_amd"),
+                        os.path.join(ROOT, "tests"), json.dumps(STAGE_CASES)],
                        capture_output=True, text=True, env=env, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     counted = json.loads(r.stdout.strip().splitlines()[-1])
     for (cname, camname, W, H), cnt in zip(STAGE_CASES, counted):
-        c = configs.CONFIGS[cname]
-        bh, dk, cfg = c.scene()
+        bh, dk, cfg, method, flags = _stage_scene(cname)
         bhrt_lib.stats(reset=True)
-        f = bhrt_lib.render_frame(bh, dk, cfg, configs.camera(camname), W, H, c.method, c.flags)
+        f = bhrt_lib.render_frame(bh, dk, cfg, configs.camera(camname), W, H, method, flags)
         st = bhrt_lib.stats(reset=True)
         what = f"{cname}/{camname} {W}x{H}"
         derived = {k: st[k] for k in cnt["stats"]}
         assert derived == cnt["stats"], (what, derived, cnt["stats"])
-        per_stage = 4 if c.method == abi.INTEGRATOR_RK4 else 6
+        per_stage = 4 if method == abi.INTEGRATOR_RK4 else 6
         assert sum(st[k] for k in ("stages_full", "stages_far", "stages_kerr")) == \
             per_stage * st["iterations"], what
         for k, v in f.items():
             assert v.tobytes().hex() == cnt["frame"][k], (what, k)
-    # the far-field camera takes both branches (a real split, not one branch for all)
-    c2v = counted[STAGE_CASES.index(("C2", "V", 96, 54))]["stats"]
-    assert c2v["stages_far"] > 0 and c2v["stages_full"] > 0, c2v
+    # the far-field scene takes both branches (a real split, not one branch for all)
+    far = counted[STAGE_CASES.index(("FAR", "B", 64, 36))]["stats"]
+    assert far["stages_far"] > 0 and far["stages_full"] > 0, far
 
 
 @pytest.mark.parametrize("cname,camname,W,H", STAGE_CASES)
@@ -1019,29 +1031,38 @@ def test_redo_pass_left_out_where_no_ray_can_need_it(bhrt_lib, monkeypatch, cnam
                                                      H):
     """bhrt_api.c origin_no_evict proves from the scene and the shared origin that no ray of a
     camera frame can be handed to the redo pass, and the launcher then leaves that launch out
-    (VERDICT r4 item 4). With the launch forced back (BHRT_SKIP_REDO=0) it must find nothing to
-    re-trace, and the frame must be the same bit for bit; a ray array with one shared origin is
-    proved the same way, an array of distinct origins is not."""
-    c = configs.CONFIGS[cname]
-    bh, dk, cfg = c.scene()
+     -- on every BASELINE frame (camera B); the bound is conservative, so a
+    scene it cannot prove (RKF45 from camera V's far origin) keeps the launch. With the launch
+    forced back (BHRT_SKIP_REDO=0) it must find nothing to re-trace, and the frame must be the
+    same bit for bit; a ray array with one shared origin is proved the same way, an array of
+    distinct origins is not."""
+    bh, dk, cfg, method, flags = _stage_scene(cname)
     cam = configs.camera(camname)
     frames = []
+    skipped = None
     for skip in ("1", "0"):
         monkeypatch.setenv("BHRT_SKIP_REDO", skip)
         bhrt_lib.stats(reset=True)
-        frames.append(bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags))
+        frames.append(bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, method, flags))
         st = bhrt_lib.stats(reset=True)
         assert st["rays_redone"] == 0, (skip, st)
-        assert st["redo_launches"] == (0 if skip == "1" else st["launches"]), (skip, st)
+        if skip == "1":
+            skipped = st["redo_launches"] == 0
+            assert skipped or st["redo_launches"] == st["launches"], st
+        else:
+            assert st["redo_launches"] == st["launches"], st
+    if camname == "B":
+        assert skipped, f"{cname}: the BASELINE frame should be proved eviction-free"
     for k in frames[0]:
         assert np.array_equal(frames[0][k], frames[1][k], equal_nan=True), k
     monkeypatch.setenv("BHRT_SKIP_REDO", "1")
     rays = configs.camera_rays(cam, W, H)
     bhrt_lib.stats(reset=True)
-    bhrt_lib.trace_rays(rays, bh, dk, cfg, c.method, c.flags)
-    assert bhrt_lib.stats(reset=True)["redo_launches"] == 0
+    bhrt_lib.trace_rays(rays, bh, dk, cfg, method, flags)
+    st = bhrt_lib.stats(reset=True)
+    assert st["redo_launches"] == (0 if skipped else st["launches"]), st
     rays["origin"][1::2, 0] += 1e-3  # two origins: per-ray set-up, not provable here
     bhrt_lib.stats(reset=True)
-    bhrt_lib.trace_rays(rays, bh, dk, cfg, c.method, c.flags)
+    bhrt_lib.trace_rays(rays, bh, dk, cfg, method, flags)
     st = bhrt_lib.stats(reset=True)
     assert st["redo_launches"] == st["launches"] > 0, st

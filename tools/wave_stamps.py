@@ -26,7 +26,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "raytracing-engine-in-c_amd"))
 
-SLOTS, WAVES, WORDS = 64, 8192, 6
+SLOTS, WAVES, WORDS = 64, 8192, 8
 # bench.py's hardware-queue setting (read when HIP initialises)
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
@@ -148,6 +148,16 @@ def analyse(path):
     dur = np.concatenate([(r[:, 1] - r[:, 0]) for r in recs]) * tick_us
     li = np.concatenate([r[:, 4] for r in recs])
     trips = np.concatenate([r[:, 3] & 0xffffffff for r in recs])
+    dur = np.concatenate([(r[:, 1] - r[:, 0]) for r in recs]) * tick_us
+    if recs[0].shape[1] >= 8:
+        ct = np.concatenate([r[:, 6] & ((1 << 48) - 1) for r in recs]) * tick_us
+        cn = np.concatenate([r[:, 6] >> 48 for r in recs])
+        first = np.concatenate([r[:, 7] for r in recs]) * tick_us
+        print(f"  claims (returning atomics) per wave {cn.mean():.2f}; time in them per wave mean "
+              f"{ct.mean():.1f} us ({ct.sum() / max(dur.sum(), 1e-9) * 100:.1f}% of wave time); "
+              f"first claim p50 {np.median(first):.2f} / p90 {np.percentile(first, 90):.2f} / max "
+              f"{first.max():.2f} us; later claims mean "
+              f"{(ct - first).sum() / max((cn - 1).clip(0).sum(), 1):.2f} us")
     print(f"  per wave: duration mean {dur.mean():.1f} us (p10 {np.percentile(dur, 10):.1f}, "
           f"p90 {np.percentile(dur, 90):.1f}), lane-iterations mean {li.mean():.0f}, "
           f"trips mean {trips.mean():.1f}; us per trip {dur.sum() / trips.sum():.3f}")
