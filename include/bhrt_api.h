@@ -357,7 +357,11 @@ void bhrt_set_refill_threshold(int lanes);
  * or -1 (and the default order) if it is not. It applies only to device-API frames of exactly
  * n rays on the device that was current here, never to the chunks of bhrt_render_frame[_async]
  * host frames. libbhrt keeps the pointer: it must stay valid until the order is cleared
- * (bhrt_set_claim_order(NULL, 0)) or replaced. */
+ * (bhrt_set_claim_order(NULL, 0)) or replaced. The check is a blocking copy on the legacy null
+ * stream, which is NOT ordered after work on non-blocking streams (torch's, libbhrt's own):
+ * synchronise the stream that wrote d_order before this call. The check costs a D2H copy, a
+ * host sync and an O(n) scan per call; BHRT_TRUST_CLAIM_ORDER=1 skips it (the caller then
+ * guarantees a permutation). Returns int since round 4 (void before). */
 int bhrt_set_claim_order(const int* d_order, int n);
 
 /* update_particles (particle_sim.c:505-566) applied `steps` times in one device round trip:

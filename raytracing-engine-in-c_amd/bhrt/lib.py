@@ -108,6 +108,9 @@ def _one_hip_runtime():
         import torch  # noqa: F401
     except ImportError:
         pass
+    except Exception as e:  # a broken torch (its bundled HIP runtime failed to load): go on
+        import warnings     # with /opt/rocm's runtime, which libbhrt finds by its SONAME
+        warnings.warn(f"torch failed to import ({e!r}); libbhrt binds /opt/rocm's HIP runtime")
 
 
 def load(path=None):

@@ -177,6 +177,7 @@ static int g_refill = 0; /* 0: chosen per scene (refill_default) */
 static __thread const int* g_order;
 static __thread int g_order_n, g_order_dev = -1;
 static int current_device(void);
+static int env_int(const char* name, int dflt);
 int bhrt_set_claim_order(const int* d_order, int n) {
     g_order = NULL;
     g_order_n = 0;
@@ -186,6 +187,12 @@ int bhrt_set_claim_order(const int* d_order, int n) {
     if (dev < 0) {
         set_err("bhrt_set_claim_order: no current HIP device");
         return -1;
+    }
+    if (env_int("BHRT_TRUST_CLAIM_ORDER", 0)) { /* the caller guarantees a permutation */
+        g_order = d_order;
+        g_order_n = n;
+        g_order_dev = dev;
+        return 0;
     }
     /* claim_ray indexes the outputs with order[position]: only a permutation is safe */
     int* h = (int*)malloc((size_t)n * sizeof(int));
@@ -651,6 +658,7 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
     kp->colour_fused = colour_fused((int)method, dk != NULL, bh->spin != 0.0);
     kp->skip_redo = env_int("BHRT_SKIP_REDO", 1) != 0;
     kp->block_lanes = env_int("BHRT_TRACE_BLOCK", 256);
+    kp->grid_div = env_int("BHRT_GRID_DIV", 1);
     kp->cam.rows.row_block = 1;
     kp->cam.rows.num_shards = 1;
     return 0;

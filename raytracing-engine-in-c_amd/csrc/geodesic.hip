@@ -1276,6 +1276,9 @@ __device__ __forceinline__ void store_colour(const bhrt_frame_soa& s, int i, dou
 #ifndef BHRT_UNIFORM_TRIP
 #define BHRT_UNIFORM_TRIP 0
 #endif
+#ifndef BHRT_DEFER_STORE
+#define BHRT_DEFER_STORE 1
+#endif
 typedef const __attribute__((address_space(4))) bhrt_kparams kparams_as4;
 // (k_trace's only argument: it starts the kernel argument segment)
 __device__ __forceinline__ const bhrt_kparams& cold(const bhrt_kparams&) {
@@ -1502,6 +1505,14 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         s_q[wv][3] = 0u;
     }
     constexpr bool COLD = BHRT_COLD_KP;
+    // Deferred stores (drained-refill instantiations): a ray that finishes keeps its final state
+    // in its lane's registers (the lane takes no new ray before the wave's next refill) and is
+    // stored AT that refill, together with every other lane that finished meanwhile -- where a
+    // wave refills only once drained (C3, C4, C5), all 64 lanes store at once, full lines of
+    // every field, instead of a few lanes per trip (partial lines, written to HBM more than once:
+    // C3's traffic was 1.40x its output) -- and the trip loop has no store code in it.
+    constexpr bool DEFER = MULTIQ && !HUGE && BHRT_DEFER_STORE;
+    int pterm = T_NONE;  // DEFER: how this lane's finished ray ended (T_NONE: nothing pending)
     bool exhausted = false;  // no ids left to claim or hand out; wave-uniform
     const HSel hsel = hsel_of<hsel_vgpr<METHOD, DISK, SPIN0>()>(kp.sc);
     for (;;) {
@@ -1513,6 +1524,10 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
 #if BHRT_WAVE_STAMPS
             st_refills++;
 #endif
+            if constexpr (DEFER) {
+                if (pterm != T_NONE) store_ray<METHOD, DISK, SPIN0>(kc, rid, R, pterm);
+                pterm = T_NONE;
+            }
             bool ok;
             unsigned long long id;
             if constexpr (MULTIQ) {
@@ -1656,7 +1671,12 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             n_live = __popcll(__ballot(live));
         }
         if (n_live == 0) {
-            if (exhausted) break;
+            if (exhausted) {
+                if constexpr (DEFER) {
+                    if (pterm != T_NONE) store_ray<METHOD, DISK, SPIN0>(kc, rid, R, pterm);
+                }
+                break;
+            }
             continue;
         }
 #if BHRT_WAVE_STAMPS
@@ -1691,7 +1711,10 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 kp.redo[atomicAdd(kp.ctl + 6, 1ull)] = rid;
                 live = false;
             } else if (term != T_NONE) {
-                store_ray<METHOD, DISK, SPIN0>(kc, rid, R, term);
+                if constexpr (DEFER)
+                    pterm = term;
+                else
+                    store_ray<METHOD, DISK, SPIN0>(kc, rid, R, term);
                 live = false;
             }
         }
@@ -1887,6 +1910,7 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
         grid_huge[dev].store(cap_huge, std::memory_order_relaxed);
     }
     int blocks = (kp.n + lanes - 1) / lanes;
+    if (kp.grid_div > 1) cap = cap / kp.grid_div > 0 ? cap / kp.grid_div : 1;
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     bhrt_kparams k = kp;
