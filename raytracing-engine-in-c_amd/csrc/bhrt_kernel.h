@@ -124,7 +124,9 @@ typedef struct {
                              (the AoS rays' direction field, stride 6, or packed, stride 3,
                              with rays NULL) */
     int dir_stride;
-    int grid_div;         /* the hot launch takes 1 / grid_div of the resident workgroups (>= 1) */
+    int grid_div;         /* > 0: the hot launch takes 1 / grid_div of the resident workgroups */
+    int min_tiles;        /* drained-refill launches: at least this many 64-ray tiles per wave
+                             (fewer waves than resident for a small launch; 0 = off) */
     int diag_slot;        /* the launch's control-block slot (the BHRT_WAVE_STAMPS diagnostic
                              build records per-wave stamps under it; unused otherwise) */
 } bhrt_kparams;

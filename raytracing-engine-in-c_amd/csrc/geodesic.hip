@@ -955,6 +955,10 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
             k = (r < sc.rs_x5) ? 2 : k;
             k = (r < sc.rs_x2_5) ? 3 : k;
             R.h = k == 0 ? hs.far_ : (k == 1 ? hs.r15 : (k == 2 ? hs.r5 : hs.r2_5));
+            // (indexed by the per-lane k these are vector loads from the kernel-argument segment,
+            // in this rare branch only; selects of the eight bounds as register values instead
+            // measured C4 +-0, C5 -1.5% same-box -- more SGPR spills around the loop --
+            // profiles/r05/ab_session_l.txt)
             R.h_lo = sc.h_lo[k];
             R.h_hi = sc.h_hi[k];
             if constexpr (rotation_trig<METHOD, SPIN0, FAR, HUGE>()) {
@@ -1910,7 +1914,22 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
         grid_huge[dev].store(cap_huge, std::memory_order_relaxed);
     }
     int blocks = (kp.n + lanes - 1) / lanes;
-    if (kp.grid_div > 1) cap = cap / kp.grid_div > 0 ? cap / kp.grid_div : 1;
+    // Waves of a drained-refill launch (C3, C4, C5) get their work in guided blocks whose first
+    // claim is the queue's size / its waves, so a launch of few tiles per wave is partitioned
+    // almost statically at its start and ends with the waves that drew the costliest tiles
+    // (a strong-scaled C4 shard: ~4 tiles per wave, trips per wave from 12 to 46,
+    // profiles/r05/c4_shard_wave_stamps.txt). Such a launch takes fewer waves -- at least
+    // min_tiles 64-ray tiles per wave -- and shares the chip with the next frames' launches:
+    // C4 8-GPU shard 0.146 -> 0.127 ms same-box (half the grid; a third the same), while launches
+    // of >= 16 tiles per wave lose 6-7% at half the grid (profiles/r05/ab_grid_fraction.txt).
+    // kp.grid_div > 0 overrides (BHRT_GRID_DIV).
+    if (kp.grid_div > 0) {
+        cap = cap / kp.grid_div > 0 ? cap / kp.grid_div : 1;
+    } else if (!(METHOD == INTEGRATOR_RK4 && SPIN0) && kp.min_tiles > 0) {  // (MULTIQ)
+        const long waves = ((long)kp.n + 64L * kp.min_tiles - 1) / (64L * kp.min_tiles);
+        const long want = (waves + lanes / 64 - 1) / (lanes / 64);
+        if (want < cap) cap = want > 0 ? (int)want : 1;
+    }
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     bhrt_kparams k = kp;
