@@ -399,7 +399,8 @@ def main():
         parallelism = (f"{'single GPU' if world == 1 else f'dp{world}'}: rank r renders shard r "
                        f"of {S} (cyclic {B}-row blocks)" +
                        ("" if world == 1 else
-                        f", one RCCL gather of the {args.gather} fields to rank 0 per frame "
+                        f", one {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
+                        f"gather of the {args.gather} fields to rank 0 per frame "
                         "(overlapped with the next frame)"))
     out = {
         "metric": METRIC,
