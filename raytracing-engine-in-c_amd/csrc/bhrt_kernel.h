@@ -125,8 +125,8 @@ typedef struct {
                              with rays NULL) */
     int dir_stride;
     int grid_div;         /* > 0: the hot launch takes 1 / grid_div of the resident workgroups */
-    int min_tiles;        /* drained-refill launches: at least this many 64-ray tiles per wave
-                             (fewer waves than resident for a small launch; 0 = off) */
+    int min_tiles;        /* drained-refill launches of fewer 64-ray tiles per resident wave
+                             than this take half the grid (0 = off) */
     int diag_slot;        /* the launch's control-block slot (the BHRT_WAVE_STAMPS diagnostic
                              build records per-wave stamps under it; unused otherwise) */
 } bhrt_kparams;

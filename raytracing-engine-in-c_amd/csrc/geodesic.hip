@@ -1918,17 +1918,17 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     // claim is the queue's size / its waves, so a launch of few tiles per wave is partitioned
     // almost statically at its start and ends with the waves that drew the costliest tiles
     // (a strong-scaled C4 shard: ~4 tiles per wave, trips per wave from 12 to 46,
-    // profiles/r05/c4_shard_wave_stamps.txt). Such a launch takes fewer waves -- at least
-    // min_tiles 64-ray tiles per wave -- and shares the chip with the next frames' launches:
-    // C4 8-GPU shard 0.146 -> 0.127 ms same-box (half the grid; a third the same), while launches
-    // of >= 16 tiles per wave lose 6-7% at half the grid (profiles/r05/ab_grid_fraction.txt).
+    // profiles/r05/c4_shard_wave_stamps.txt). Such a launch -- fewer than min_tiles 64-ray
+    // tiles per wave on the resident grid -- takes half the grid and shares the chip with the
+    // next frames' launches: C4 8-GPU shard 0.146 -> 0.127 ms, 4-GPU shard +3.6% same-box,
+    // while launches of >= 16 tiles per wave lose 6-7% at half the grid (C3, C4 full, C5) and a
+    // quarter grid loses against a half (profiles/r05/ab_grid_fraction.txt, ab_min_tiles.txt).
     // kp.grid_div > 0 overrides (BHRT_GRID_DIV).
     if (kp.grid_div > 0) {
         cap = cap / kp.grid_div > 0 ? cap / kp.grid_div : 1;
-    } else if (!(METHOD == INTEGRATOR_RK4 && SPIN0) && kp.min_tiles > 0) {  // (MULTIQ)
-        const long waves = ((long)kp.n + 64L * kp.min_tiles - 1) / (64L * kp.min_tiles);
-        const long want = (waves + lanes / 64 - 1) / (lanes / 64);
-        if (want < cap) cap = want > 0 ? (int)want : 1;
+    } else if (!(METHOD == INTEGRATOR_RK4 && SPIN0) && kp.min_tiles > 0 &&  // (MULTIQ)
+               (long)kp.n < 64L * kp.min_tiles * (long)cap * (lanes / 64)) {
+        cap = (cap + 1) / 2;
     }
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
