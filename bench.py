@@ -7,7 +7,7 @@ the rendering of frame i+1, and the timed region ends after the last one). Conse
 alternate between HIP streams, so the workgroups of frame i+1 take the CUs that frame i's tail
 -- its last, longest rays draining -- leaves idle (tools/wave_tail.py: ~9% of a lone C2
 launch): two streams, or four for short frames (--streams auto, the default: a frame under
-0.4 ms, or too few rays to fill the chip's resident waves); --streams 1 runs them back to back.
+0.6 ms, or too few rays to fill the chip's resident waves); --streams 1 runs them back to back.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--camera B]
 
@@ -126,7 +126,7 @@ CPU_ROWS_STRIDE = {"C1": 1, "C2": 27, "C3": 27, "C4": 4, "C5": 3}
 # --streams auto: four frames in flight instead of two when a frame is short or small. Same-box
 # A/B (profiles/r04/session_f_streams/run2_warmed.txt): 4 streams C1 +6.5%, C3 +4.5%, the C4 8-GPU-plan
 # shard 0.186 -> 0.157 ms; C2 -1%, C4 full frame -1%, C5 -2%.
-AUTO_SHORT_MS = 0.4
+AUTO_SHORT_MS = 0.6
 AUTO_FILL_RAYS = 256 * 4 * 4 * 64  # 4 waves per SIMD x 4 SIMDs x 256 CUs x 64 lanes
 
 

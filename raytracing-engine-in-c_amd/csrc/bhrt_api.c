@@ -659,6 +659,7 @@ static int fill_scene(bhrt_kparams* kp, const BlackHoleParams* bh, const Accreti
     kp->skip_redo = env_int("BHRT_SKIP_REDO", 1) != 0;
     kp->block_lanes = env_int("BHRT_TRACE_BLOCK", 256);
     kp->grid_div = env_int("BHRT_GRID_DIV", 0);
+    kp->grid_blocks = env_int("BHRT_GRID_BLOCKS", 0);
     kp->min_tiles = env_int("BHRT_MIN_TILES", 10);
     kp->cam.rows.row_block = 1;
     kp->cam.rows.num_shards = 1;

@@ -125,6 +125,7 @@ typedef struct {
                              with rays NULL) */
     int dir_stride;
     int grid_div;         /* > 0: the hot launch takes 1 / grid_div of the resident workgroups */
+    int grid_blocks;      /* > 0: at most this many workgroups in the hot launch (A/B knob) */
     int min_tiles;        /* drained-refill launches of fewer 64-ray tiles per resident wave
                              than this take half the grid (0 = off) */
     int diag_slot;        /* the launch's control-block slot (the BHRT_WAVE_STAMPS diagnostic

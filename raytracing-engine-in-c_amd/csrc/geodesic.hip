@@ -1394,8 +1394,9 @@ __global__ __launch_bounds__(256) void k_init(const bhrt_kparams kp) {
 //  * RKF45, a != 0, no disk (C5): 4. Since v23's two attempts per loop trip, 5 waves spill
 //    (96 VGPRs + 156 B scratch) and 4 waves is best: +8.5% over 5, 6 loses 27%
 //    (profiles/r02_ab_v23_occupancy.txt).
-//  * C3 (RKF45 a = 0 disk) and C4 (RK4 Kerr disk) keep the compiler's choice: forcing one
-//    more wave spills in their hot blocks (-14%, -1.5%).
+//  * C3 (RKF45 a = 0 disk): 3 (round 5: 168 VGPRs without spills), with launches of two waves
+//    per SIMD (trace_launch_waves). C4 (RK4 Kerr disk) keeps the compiler's choice: 5 waves
+//    spill (96 VGPRs + 84 B scratch) and gain nothing even with a capped grid.
 // step sizes in VGPRs (hsel_of): the RK4 disk instantiations. C4 (Kerr, ~100 VGPRs) has the
 // room; C2 (a = 0, capped at 128) gives its rare-lane blocks a few more spills but its iteration
 // loses 7 v_mov_b32 (an SGPR operand of v_cndmask next to VCC exceeds gfx9's one constant-bus
@@ -1412,6 +1413,24 @@ constexpr int trace_waves() {
          : (METHOD == INTEGRATOR_RK4 && SPIN0) ? 4
          : 0;
 }
+// the C3 camera kernel (RKF45, a = 0, disk, in-kernel set-up, near field) at 3 waves per SIMD;
+// its other instantiations (ray arrays, far field, the redo pass) keep the compiler's choice
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, int INL>
+constexpr bool c3_camera() {
+    return METHOD == INTEGRATOR_RKF45 && DISK && SPIN0 && !FAR && !HUGE && INL == 1;
+}
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, int INL>
+constexpr int trace_waves_k() {
+    return c3_camera<METHOD, DISK, SPIN0, FAR, HUGE, INL>() ? 3 : trace_waves<METHOD, DISK, SPIN0>();
+}
+// Waves per SIMD ONE hot launch takes (0: every resident slot). C3 is resident at 3 waves per
+// SIMD (168 VGPRs, no spills) but launches 2 per SIMD's worth: the frames in flight fill the third
+// slot. A full 3-wave grid deals each wave ~10 blocks in its first (static) claim and loses 10%
+// against the 2-wave kernel; the 2-of-3 grid keeps ~16 blocks per wave and gains 11.6% (C3 13.1
+// -> 14.6 Grays/s same-box; 448 / 576 blocks +8% / -6%, profiles/r05/ab_occupancy_grid.txt).
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, int INL>
+constexpr int trace_launch_waves() {
+    return c3_camera<METHOD, DISK, SPIN0, FAR, false, INL>() ? 2 : 0;}
 constexpr int BHRT_TRACE_WAVES_PER_BLOCK = 4;
 
 // Ray queues of k_trace: 64-id block b of the launch belongs to queue b mod 2^qbits; queue q's
@@ -1424,7 +1443,7 @@ __device__ __forceinline__ unsigned queue_size(unsigned ntotal, unsigned qbits, 
     return (((nb >> qbits) + (q < last ? 1u : 0u)) << 6) + (q == last ? (ntotal & 63u) : 0u);
 }  // k_trace launches 256-lane workgroups
 #define BHRT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, 256), \
-                                         amdgpu_waves_per_eu(trace_waves<METHOD, DISK, SPIN0>() > 0 ? trace_waves<METHOD, DISK, SPIN0>() : 1)))
+                                         amdgpu_waves_per_eu(trace_waves_k<METHOD, DISK, SPIN0, FAR, HUGE, INL>() > 0 ? trace_waves_k<METHOD, DISK, SPIN0, FAR, HUGE, INL>() : 1)))
 
 // Diagnostic build only (make DEFS=-DBHRT_WAVE_STAMPS=1, tools/wave_stamps.py): every wave of a
 // hot k_trace launch records, under the launch's control-block slot, its start and end on the
@@ -1924,7 +1943,13 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     // while launches of >= 16 tiles per wave lose 6-7% at half the grid (C3, C4 full, C5) and a
     // quarter grid loses against a half (profiles/r05/ab_grid_fraction.txt, ab_min_tiles.txt).
     // kp.grid_div > 0 overrides (BHRT_GRID_DIV).
-    if (kp.grid_div > 0) {
+    if (trace_launch_waves<METHOD, DISK, SPIN0, FAR, INL>() > 0 && kp.grid_blocks <= 0) {
+        const int lw = device_cus(dev) * trace_launch_waves<METHOD, DISK, SPIN0, FAR, INL>() * 4 / (lanes / 64);
+        if (lw > 0 && lw < cap) cap = lw;
+    }
+    if (kp.grid_blocks > 0) {  // (A/B: an absolute grid, BHRT_GRID_BLOCKS)
+        cap = kp.grid_blocks < cap ? kp.grid_blocks : cap;
+    } else if (kp.grid_div > 0) {
         cap = cap / kp.grid_div > 0 ? cap / kp.grid_div : 1;
     } else if (!(METHOD == INTEGRATOR_RK4 && SPIN0) && kp.min_tiles > 0 &&  // (MULTIQ)
                (long)kp.n < 64L * kp.min_tiles * (long)cap * (lanes / 64)) {
