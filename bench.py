@@ -143,8 +143,14 @@ def parse():
                         "per config, ~1-3 s on 16 cores: CPU_ROWS_STRIDE)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-path", action="store_true",
-                   help="skip the host-buffer leg (its chunked launches would mix into a "
+                   help="skip the extra legs after the timed frames: host-buffer frames and "
+                        "the display-only resident frames (their launches would mix into a "
                         "profiler's per-launch kernel averages)")
+    p.add_argument("--fields", choices=("all", "display"), default="all",
+                   help="what each timed frame writes: every SoA field + rgba8 (100 B/ray, "
+                        "default; the CPU baseline compares them) or the visualizer's display "
+                        "call, rgba8 alone (plus result / hit_x / hit_y where the colour is a "
+                        "separate pass: Config.display_fields)")
     p.add_argument("--streams", default="auto",
                    help="consecutive frames alternate between this many HIP streams (1-4; "
                         "one frame buffer each), so the next frames' rays fill the CUs the tail "
@@ -274,6 +280,11 @@ def main():
         args.gather = "image"  # (samples mode averages the f64 colour planes)
     gather = {"all": None, "image": RGB_FIELDS, "rgba8": DISPLAY_FIELD}[args.gather]
     fields = FIELDS + DISPLAY_FIELD if args.gather == "rgba8" else FIELDS
+    if args.fields == "display":
+        if samples:
+            raise SystemExit("--fields display: tiles mode only (samples average f64 colour)")
+        fields, gather = c.display_fields(), DISPLAY_FIELD
+        args.no_cpu_baseline = True  # (no hit fields to compare)
     pipe = FramePipeline(n, device, world, rank, "samples" if samples else "shards", H, W, B,
                          fields, shards=S, gather=gather, first_shard=shard - rank,
                          slots=4 if auto else nstreams)
@@ -430,6 +441,7 @@ def main():
             "row_block": B,
             "rays_per_frame": rays_frame,
             "rays_per_gpu": rays_frame // world if not samples else W * H,
+            "fields": list(fields),
             "parallelism": parallelism,
         },
         "rk4_steps_per_s": round(iterations_all * (1.0 / elapsed), 1),
@@ -497,6 +509,10 @@ def main():
                        "process group's own events (TORCH_NCCL_ENABLE_TIMING; not measured "
                        "with gloo)"),
         }
+    if world == 1 and not args.no_host_path and args.fields == "all":
+        out["display_resident"] = display_resident_rate(
+            c, bh, dk, cfg, cam, W, H, rows, n, rays_frame, streams[:active[0]], device,
+            args.steps)
     if world == 1 and not args.no_host_path and S == 1:  # (bhrt_render_frame: whole images)
         out["host_path"] = host_path_rate(c, bh, dk, cfg, cam, W, H)
     if world == 1 and not args.no_cpu_baseline:
@@ -530,6 +546,44 @@ def prev_tiles_order(pipe, last, H, W, B, S, shard):
     torch.cuda.synchronize()
     lib.set_claim_order(perm.data_ptr(), nrows * W)
     return perm
+
+
+def display_resident_rate(c, bh, dk, cfg, cam, W, H, rows, n, rays, streams, device, frames):
+    """The same frames as the timed region, on the same streams, writing only the display
+    call's device fields (Config.display_fields: 4 B/ray on C3/C4, 24 B/ray elsewhere)
+    instead of every SoA field: the resident rate of a renderer that only shows the image.
+    Reported beside `value`, never as it."""
+    fields = c.display_fields()
+    nb = max(2, len(streams))
+    bufs = [{f: torch.empty((n, 4) if f == "rgba8" else (n,),
+                            dtype={"rgba8": torch.uint8, "result": torch.int32}.get(
+                                f, torch.float64), device=device) for f in fields}
+            for _ in range(nb)]
+    soas = [lib.soa_from_tensors(b) for b in bufs]
+    torch.cuda.synchronize()
+
+    def issue(k):  # buffer k % nb is only ever used on stream k % len(streams)
+        s = streams[k % len(streams)]
+        lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags, soas[k % nb],
+                                s.cuda_stream)
+
+    for k in range(2 * nb):
+        issue(k)
+    torch.cuda.synchronize()
+    lib.stats(reset=True)
+    t0 = time.perf_counter()
+    for k in range(frames):
+        issue(k)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / frames
+    st = lib.stats(reset=True)
+    return {"mrays_s": round(rays / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 3),
+            "fields": list(fields),
+            "bytes_per_ray": sum(4 if f in ("rgba8", "result") else 8 for f in fields),
+            "kernel_span_ms_per_frame": round(st["span_ms"] / max(st["launches"], 1), 4),
+            "streams": len(streams),
+            "note": "device-resident frames like the timed ones, writing only the display "
+                    "call's fields (bench.py --fields display times them as the main line)"}
 
 
 def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):

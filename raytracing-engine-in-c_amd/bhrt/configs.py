@@ -126,6 +126,14 @@ class Config:
                          f"{W}x{H} frame ({n} x the {self.width}x{self.height} rays at its "
                          f"aspect and field of view) in {n} shards")
 
+    def display_fields(self):
+        """The device fields of the visualizer's display call: rgba8 alone where the trace
+        kernel writes the colour at each ray's exit (bhrt_kernel.h BHRT_COLOUR_IN_TRACE: a disk
+        scene traced with RKF45, or with RK4 at a != 0: C3, C4), else also result and the hit
+        point that the separate colour pass reads (bhrt_api.c colour_args_bad)."""
+        fused = self.disk and (self.method == abi.INTEGRATOR_RKF45 or self.spin != 0.0)
+        return ("rgba8",) if fused else ("result", "hit_x", "hit_y", "rgba8")
+
     def scene(self):
         bh = abi.black_hole(1.0, self.spin)
         dk = abi.disk(bh.isco_radius, 20.0, 1.0, 1.0) if self.disk else None

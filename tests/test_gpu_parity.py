@@ -613,6 +613,37 @@ def test_display_path_rgba(bhrt_lib, oracle, monkeypatch, cname, fuse):
     assert np.abs(got["rgba8"][:, :3].astype(int) - _display_u8(w32).astype(int)).max() <= 1
 
 
+@pytest.mark.parametrize("cname", ["C1", "C2", "C3", "C4", "C5"])
+def test_display_fields_device_frame(bhrt_lib, cname):
+    """bench.py's display_resident leg (and --fields display): a device frame that asks only
+    for Config.display_fields() -- rgba8 alone where the colour is written in the trace
+    kernel -- is accepted and gives the rgba8 of the every-field frame bit for bit."""
+    import torch
+    c = configs.CONFIGS[cname]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera("B")
+    W, H = 96, 54
+    n = W * H
+
+    def frame(fields):
+        t = {f: torch.full((n, 4) if f == "rgba8" else (n,), 7,
+                           dtype={"rgba8": torch.uint8, "result": torch.int32,
+                                  "steps": torch.int32}.get(f, torch.float64), device="cuda")
+             for f in fields}
+        torch.cuda.synchronize()
+        bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                     bhrt_lib.soa_from_tensors(t), None)
+        torch.cuda.synchronize()
+        return {f: v.cpu().numpy() for f, v in t.items()}
+
+    fused = c.display_fields() == ("rgba8",)
+    assert fused == (cname in ("C3", "C4"))
+    only = frame(c.display_fields())
+    full = frame(abi.SOA_FIELDS + ("rgba8",))
+    for f in c.display_fields():
+        assert np.array_equal(only[f], full[f], equal_nan=True), f
+
+
 def test_sub_pixel_offset_frames(bhrt_lib, oracle):
     """bhrt_camera.use_offset: frames at trace_pixel's jitter offsets (the weak-scaling sample
     planes of bench.py) against the oracle."""
