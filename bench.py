@@ -127,6 +127,11 @@ CPU_ROWS_STRIDE = {"C1": 1, "C2": 27, "C3": 27, "C4": 4, "C5": 3}
 # A/B (profiles/r04/session_f_streams/run2_warmed.txt): 4 streams C1 +6.5%, C3 +4.5%, the C4 8-GPU-plan
 # shard 0.186 -> 0.157 ms; C2 -1%, C4 full frame -1%, C5 -2%.
 AUTO_SHORT_MS = 0.6
+# Sustained load right before the timed frames ("Clock ramp"): after an
+# idle gap of a few ms the GPU's frame time falls over ~30 ms of continuous work (C4 one stream
+# 1.20 -> 0.95 ms per frame, profiles/r05/clock_ramp.txt), so the untimed frames end with this
+# many ms of back-to-back frames and the timed region follows after one sync.
+WARM_MS = float(os.environ.get("BHRT_BENCH_WARM_MS", "200"))
 AUTO_FILL_RAYS = 256 * 4 * 4 * 64  # 4 waves per SIMD x 4 SIMDs x 256 CUs x 64 lanes
 
 
@@ -345,8 +350,31 @@ def main():
                 step()
             pipe.finish()
             warmup += len(streams)
+    sustained = 0
+    if WARM_MS > 0:
+        # (frame time from one untimed round on the active streams, then frames back to back)
+        torch.cuda.synchronize()
+        tw = time.perf_counter()
+        for _ in range(active[0]):
+            step()
+        pipe.finish()
+        torch.cuda.synchronize()
+        est_ms = (time.perf_counter() - tw) / active[0] * 1e3
+        extra = min(int(WARM_MS / max(est_ms, 1e-3)) + 1, 4000)
+        if world > 1:  # every rank the same frames, started together: they end together, and
+            # the barrier below leaves no rank idle for long before its timed frames
+            t = torch.tensor([extra], dtype=torch.float64, device="cpu" if shared else device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            extra = int(t.item())
+            dist.barrier()
+        sustained = active[0] + extra
+        for _ in range(extra):
+            step()
+        pipe.finish()
+        warmup += sustained
     torch.cuda.synchronize()
-    lib.stats(reset=True)
+    t_idle = time.perf_counter()  # the GPU is idle from here to the first timed launch
+    lib.stats_discard()
     pipe.collective_ms.clear()
     if world > 1:
         dist.barrier()
@@ -461,6 +489,8 @@ def main():
                                if auto else "fixed (--streams)"),
             "iterations_per_launch": st["iterations"] / max(st["launches"], 1),
             "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 4),
+            "sustained_warmup": {"frames": sustained, "ms_asked": WARM_MS,
+                                 "idle_before_timed_ms": round((t0 - t_idle) * 1e3, 3)},
             "mean_iterations_per_ray": st["iterations"] / max(st["rays"], 1),
         },
         "roofline": {
@@ -512,7 +542,7 @@ def main():
     if world == 1 and not args.no_host_path and args.fields == "all":
         out["display_resident"] = display_resident_rate(
             c, bh, dk, cfg, cam, W, H, rows, n, rays_frame, streams[:active[0]], device,
-            args.steps)
+            args.steps, elapsed / args.steps * 1e3)
     if world == 1 and not args.no_host_path and S == 1:  # (bhrt_render_frame: whole images)
         out["host_path"] = host_path_rate(c, bh, dk, cfg, cam, W, H)
     if world == 1 and not args.no_cpu_baseline:
@@ -548,7 +578,8 @@ def prev_tiles_order(pipe, last, H, W, B, S, shard):
     return perm
 
 
-def display_resident_rate(c, bh, dk, cfg, cam, W, H, rows, n, rays, streams, device, frames):
+def display_resident_rate(c, bh, dk, cfg, cam, W, H, rows, n, rays, streams, device, frames,
+                          frame_ms):
     """The same frames as the timed region, on the same streams, writing only the display
     call's device fields (Config.display_fields: 4 B/ray on C3/C4, 24 B/ray elsewhere)
     instead of every SoA field: the resident rate of a renderer that only shows the image.
@@ -567,10 +598,10 @@ def display_resident_rate(c, bh, dk, cfg, cam, W, H, rows, n, rays, streams, dev
         lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags, soas[k % nb],
                                 s.cuda_stream)
 
-    for k in range(2 * nb):
+    for k in range(max(2 * nb, int(WARM_MS / max(frame_ms, 1e-3)) + 1)):  # (sustained: WARM_MS)
         issue(k)
     torch.cuda.synchronize()
-    lib.stats(reset=True)
+    lib.stats_discard()
     t0 = time.perf_counter()
     for k in range(frames):
         issue(k)

@@ -216,6 +216,12 @@ def stats(reset=False):
     return {f: getattr(s, f) for f, _ in abi.Stats._fields_}
 
 
+def stats_discard():
+    """bhrt_get_stats(NULL, 1): wait for this thread's launches and drop their counters unread
+    (no event timing: the cheap reset before a timed region)."""
+    _check(load().bhrt_get_stats(None, 1), "bhrt_get_stats")
+
+
 def halton(index, base):
     """halton_sequence (raytracer.c:852-863), libbhrt's host export."""
     L = load()

@@ -302,6 +302,17 @@ static devctx_t* ctx_get(int device) {
         free(c);
         return NULL;
     }
+    {   /* the harvest's strided D2H copy once here: its first use in a process loads the
+         * runtime's copy kernels (~7 ms, measured as GPU idle time before bench.py's timed
+         * frames when the first harvest came there) */
+        unsigned long long h[BHRT_CTL_WORDS];
+        if (hipMemcpy2D(h, sizeof h, c->d_ctl, BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                        sizeof h, 1, hipMemcpyDeviceToHost) != hipSuccess) {
+            set_err("cannot read the control blocks on device %d", device);
+            free(c);
+            return NULL;
+        }
+    }
     if (hipEventCreate(&c->span_ref) != hipSuccess) {
         set_err("hipEventCreate failed");
         free(c);
@@ -442,23 +453,25 @@ static hipError_t ring_zero(devctx_t* c) {
     return e != hipSuccess ? e : hipStreamSynchronize((hipStream_t)0);
 }
 
-/* fold finished launches into g_stats (waits for them) */
-static int harvest(devctx_t* c) {
+/* fold finished launches into g_stats (waits for them); fold = 0 discards them unread (no
+ * counter copy, no event timing: a caller resetting the statistics before a timed region must
+ * not leave the GPU idle for the ~0.2 ms per launch that the event queries take, bench.py) */
+static int harvest(devctx_t* c, int fold) {
     if (c->npend == 0) return 0;
     unsigned long long h[BHRT_RING * BHRT_CTL_WORDS];
     HIP_TRY(hipSetDevice(c->device));
     for (int i = 0; i < c->npend; i++) HIP_TRY(hipEventSynchronize(c->pend[i].ev1));
-    HIP_TRY(hipMemcpy2D(h, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
-                        BHRT_SLOT_WORDS * sizeof(unsigned long long),
-                        BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
-                        hipMemcpyDeviceToHost));
+    if (fold)
+        HIP_TRY(hipMemcpy2D(h, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+                            BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                            BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
+                            hipMemcpyDeviceToHost));
     /* every launch of the ring has completed: zero it for the next 64 (launch() itself issues
      * no memset -- a fill kernel per frame that had to wait for a free wave slot behind the
      * other frames' persistent kernels; a slot is reused only after it was harvested here) */
     HIP_TRY(ring_zero(c));
-    for (int i = 0; i < c->npend; i++) {
-        float ms = 0.f, t0 = 0.f, t1 = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, c->pend[i].ev0, c->pend[i].ev1));
+    for (int i = 0; fold && i < c->npend; i++) {
+        float t0 = 0.f, t1 = 0.f;  /* start and end relative to span_ref (ms) */
         HIP_TRY(hipEventElapsedTime(&t0, c->span_ref, c->pend[i].ev0));
         HIP_TRY(hipEventElapsedTime(&t1, c->span_ref, c->pend[i].ev1));
         if (t0 < c->span_lo) c->span_lo = t0;
@@ -472,7 +485,7 @@ static int harvest(devctx_t* c) {
         g_stats.rays_redone += w[6];
         g_stats.redo_launches += (uint64_t)c->pend[i].redo;
         g_stats.launches += 1;
-        g_stats.kernel_ms += ms;
+        g_stats.kernel_ms += t1 - t0;
     }
     c->npend = 0;
     return 0;
@@ -484,7 +497,7 @@ int bhrt_get_stats(bhrt_stats* out, int reset) {
     for (int d = 0; d < BHRT_MAX_DEV; d++) {
         devctx_t* c = g_ctx[d];
         if (!c) continue;
-        if (harvest(c) != 0) rc = -1;
+        if (harvest(c, out != NULL || !reset) != 0) rc = -1;
         if (c->span_on && c->span_hi > c->span_lo) span += c->span_hi - c->span_lo;
         if (reset) c->span_on = 0;
     }
@@ -748,7 +761,7 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     }
     /* the redo list follows the initial-state table (one extra field of the allocation) */
     kp->redo = (int*)(kp->init + (size_t)BHRT_INIT_FIELDS * (size_t)kp->n);
-    if (c->npend == BHRT_RING && harvest(c) != 0) return -1;
+    if (c->npend == BHRT_RING && harvest(c, 1) != 0) return -1;
     int slot = c->next_slot;
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
     kp->ctl = c->d_ctl + (size_t)slot * BHRT_SLOT_WORDS;
