@@ -10,6 +10,7 @@
 #   smoke          __graft_entry__.smoke()
 #   bench          the default bench line (bench.py, no flags)
 #   rocprof        the default bench line under rocprofv3 --kernel-trace --stats (+ trace span)
+#   rocprof_timed  the timed frames alone under rocprofv3: busy span per dispatch vs the line's avg_ms
 #   bench_all      bench.py --config C1..C5 ($CONFIGS), N = 1
 #   plan           every shard of the 8-GPU plans of $PLAN_CFGS (tools/plan_shards.sh) + summary
 #   pmc            rocprofv3 PMC passes of $PMC_CFGS (tools/pmc_all.sh)
@@ -48,6 +49,16 @@ for step in "$@"; do
     python tools/trace_span.py $(find $OUT/prof_default -name "*kernel_trace.csv" | head -1) --skip 2 \
       > $OUT/trace_span_default.txt || true
     cat $OUT/trace_span_default.txt ;;
+  rocprof_timed)
+    # like-for-like: the timed frames only (no extra legs), their busy span per dispatch from the
+    # trace against the profiled line's own kernel.avg_ms
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_timed -o run --output-format csv \
+      -- python bench.py --no-host-path --no-cpu-baseline --steps ${STEPS:-20} $BENCH_ARGS > $OUT/bench_timed_prof.json \
+      2> $OUT/prof_timed.err || fail rocprof_timed $OUT/prof_timed.err
+    python tools/trace_span.py $(find $OUT/prof_timed -name "*kernel_trace.csv" | head -1) --last ${STEPS:-20} \
+      > $OUT/trace_span_timed.txt || true
+    cat $OUT/trace_span_timed.txt
+    python3 -c "import json; d=json.load(open('$OUT/bench_timed_prof.json')); print('profiled line kernel.avg_ms', d['kernel']['avg_ms'], 'value', d['value'])" ;;
   bench_all)
     OUT=$OUT/bench_all STEPS=${STEPS:-10} CONFIGS="${CONFIGS:-C1 C2 C3 C4 C5}" bash tools/bench_all.sh \
       || fail bench_all ;;

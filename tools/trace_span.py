@@ -20,6 +20,8 @@ def main():
                          "that has the most GPU time in the trace)")
     ap.add_argument("--skip", type=int, default=0, help="leave out the first k dispatches "
                     "(bench.py's untimed warm-up frames)")
+    ap.add_argument("--last", type=int, default=0, help="keep only the last k dispatches "
+                    "(bench.py --no-host-path --steps k: its timed frames)")
     a = ap.parse_args()
     with open(a.trace) as f:
         rows = list(csv.DictReader(f))
@@ -35,6 +37,8 @@ def main():
           if a.kernel in r["Kernel_Name"]]
     iv.sort()
     iv = iv[a.skip:]
+    if a.last > 0:
+        iv = iv[-a.last:]
     n = len(iv)
     mean = sum(e - s for s, e in iv) / n
     union, cs, ce = 0, None, None
