@@ -193,6 +193,14 @@ static void run(BlackHoleParams* bh, SimulationConfig* cfg, AccretionDiskParams*
             soa_free(&h);
         }
     }
+    /* a discarding reset (bench.py's, before its timed frames) drops this thread's pending
+     * launches unread; the frames below are counted afresh */
+    {
+        bhrt_stats z;
+        CHECK(bhrt_get_stats(NULL, 1) == 0, "discarding stats reset: %s", bhrt_last_error());
+        CHECK(bhrt_get_stats(&z, 0) == 0 && z.launches == 0 && z.rays == 0 && z.kernel_ms == 0.0,
+              "stats after a discarding reset: %llu launches", (unsigned long long)z.launches);
+    }
     /* frames in flight: 5 queued (the 4th and 5th wait for the oldest slots) */
     {
         const int W = 1500, H = 900;
