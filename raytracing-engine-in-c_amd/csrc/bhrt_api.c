@@ -90,7 +90,12 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 /* device contexts                                                                          */
 /* ======================================================================================= */
 #define BHRT_MAX_DEV 16
-#define BHRT_RING 64        /* control blocks per context             */
+/* control blocks per context: a launch into a full ring first harvests it, waiting for every
+ * launch in flight -- the GPU drains once per BHRT_RING launches of a thread (C3 frames back to
+ * back: ~0.3 ms idle per harvest), so the ring is long (256 slots, 2.2 MB per context) */
+#ifndef BHRT_RING
+#define BHRT_RING 256
+#endif
 #define BHRT_CTL_WORDS 8    /* u64 per control block (64 B)           */
 #define BHRT_QWORDS ((1 << BHRT_MAX_QUEUE_BITS) * BHRT_QUEUE_STRIDE_MAX) /* queue heads per block */
 /* a launch's control block and its ray-queue heads are one region (zeroed by ONE memset per
