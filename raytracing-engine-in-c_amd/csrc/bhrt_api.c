@@ -471,7 +471,7 @@ static int harvest(devctx_t* c, int fold) {
                             BHRT_SLOT_WORDS * sizeof(unsigned long long),
                             BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
                             hipMemcpyDeviceToHost));
-    /* every launch of the ring has completed: zero it for the next 64 (launch() itself issues
+    /* every launch of the ring has completed: zero it for the next BHRT_RING (launch() itself issues
      * no memset -- a fill kernel per frame that had to wait for a free wave slot behind the
      * other frames' persistent kernels; a slot is reused only after it was harvested here) */
     HIP_TRY(ring_zero(c));
