@@ -1110,3 +1110,52 @@ def test_redo_pass_left_out_where_no_ray_can_need_it(bhrt_lib, monkeypatch, cnam
     bhrt_lib.trace_rays(rays, bh, dk, cfg, method, flags)
     st = bhrt_lib.stats(reset=True)
     assert st["redo_launches"] == st["launches"] > 0, st
+
+
+def test_control_ring_wraps(bhrt_lib):
+    """600 device frames back to back on one stream, no sync between them: the launch that
+    finds the thread's control ring full (256 slots, bhrt_api.c BHRT_RING) harvests it and
+    zeroes it, twice here. Every frame must be the first one bit for bit (a slot reused
+    without its queue heads zeroed would skip rays) and the statistics must count every launch
+    once; a discarding reset (bhrt_get_stats(NULL, 1)) drops pending launches unread."""
+    import torch
+    c = configs.CONFIGS["C2"]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera("B")
+    W, H, frames = 16, 16, 600
+    n = W * H
+
+    def bufs():
+        return {f: torch.full((n,), 7, dtype=torch.int32 if f in ("result", "steps") else
+                              torch.float64, device="cuda") for f in abi.SOA_FIELDS}
+
+    first = bufs()
+    torch.cuda.synchronize()
+    bhrt_lib.stats(reset=True)
+    bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                 bhrt_lib.soa_from_tensors(first), None)
+    torch.cuda.synchronize()
+    one = bhrt_lib.stats(reset=True)
+    assert one["launches"] == 1 and one["rays"] == n, one
+    ring = [bufs() for _ in range(3)]
+    torch.cuda.synchronize()
+    soas = [bhrt_lib.soa_from_tensors(b) for b in ring]
+    for k in range(frames):
+        bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                     soas[k % 3], None)
+    torch.cuda.synchronize()
+    st = bhrt_lib.stats(reset=True)
+    assert st["launches"] == frames and st["rays"] == frames * n, st
+    assert st["iterations"] == frames * one["iterations"], (st, one)
+    for b in ring:
+        for f in abi.SOA_FIELDS:
+            assert torch.equal(b[f], first[f]) or (
+                b[f].dtype == torch.float64 and
+                torch.equal(torch.isnan(b[f]), torch.isnan(first[f])) and
+                torch.equal(b[f].nan_to_num(0.0), first[f].nan_to_num(0.0))), f
+    for k in range(5):
+        bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                     soas[k % 3], None)
+    bhrt_lib.stats_discard()
+    st = bhrt_lib.stats(reset=True)
+    assert st["launches"] == 0 and st["rays"] == 0, st
