@@ -280,6 +280,7 @@ def test_device_api_on_torch_stream(bhrt_lib):
     s = torch.cuda.Stream()
     t = {f: torch.full((W * H,), -1, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
                        device="cuda") for f in abi.SOA_FIELDS}
+    s.wait_stream(torch.cuda.current_stream())  # (the fills ran on torch's current stream)
     with torch.cuda.stream(s):
         bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
                                      bhrt_lib.soa_from_tensors(t), s.cuda_stream)
@@ -372,6 +373,7 @@ def test_claim_order_does_not_change_results(bhrt_lib, monkeypatch, cname):
                                      order.numel() if order is not None else 0)
             t = {f: torch.full((n,), -1, dtype=torch.int32 if f in ("result", "steps")
                                else torch.float64, device="cuda") for f in abi.SOA_FIELDS}
+            torch.cuda.synchronize()  # (torch fills on its stream, libbhrt renders on its own)
             bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
                                          bhrt_lib.soa_from_tensors(t), 0)
             torch.cuda.synchronize()
@@ -670,6 +672,7 @@ def test_host_frame_chunks_equal_device_frame(bhrt_lib, monkeypatch):
     W, H = 640, 416
     t = {f: torch.zeros(W * H, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
                         device="cuda") for f in abi.SOA_FIELDS}
+    torch.cuda.synchronize()  # (torch fills on its stream, libbhrt renders on its own)
     bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
                                  bhrt_lib.soa_from_tensors(t), 0)
     torch.cuda.synchronize()
@@ -758,6 +761,9 @@ def test_full_frame_every_ray_vs_oracle(bhrt_lib, oracle, cname):
     n = W * (H if rows is None else bhrt_lib.shard_rows(H, rows))
     t = {f: torch.zeros(n, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
                         device="cuda") for f in abi.SOA_FIELDS}
+    # torch zero-fills on its stream, libbhrt renders on its own non-blocking one: without this
+    # sync a fill still queued behind the trace kernel's resident waves overwrites its output
+    torch.cuda.synchronize()
     bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags,
                                  bhrt_lib.soa_from_tensors(t), 0)
     torch.cuda.synchronize()
@@ -790,6 +796,7 @@ def test_frames_with_freed_arrays_and_pageable_copies(bhrt_lib, monkeypatch):
     for cam in cams:
         t = {f: torch.zeros(W * H, dtype=torch.int32 if f in ("result", "steps") else
                             torch.float64, device="cuda") for f in abi.SOA_FIELDS}
+        torch.cuda.synchronize()  # (torch fills on its stream, libbhrt renders on its own)
         bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
                                      bhrt_lib.soa_from_tensors(t), 0)
         torch.cuda.synchronize()

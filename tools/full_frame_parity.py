@@ -38,6 +38,7 @@ def gpu_frame(c, bh, dk, cfg, cam, W, H, rows):
     n = W * (H if rows is None else lib.shard_rows(H, rows))
     t = {f: torch.zeros(n, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
                         device="cuda") for f in abi.SOA_FIELDS}
+    torch.cuda.synchronize()  # (torch fills on its stream, libbhrt renders on its own)
     lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags,
                             lib.soa_from_tensors(t), 0)
     torch.cuda.synchronize()
