@@ -276,7 +276,10 @@ int bhrt_shard_rows(int height, const bhrt_rows* rows);
 
 /* Render (a shard of) a camera frame into DEVICE SoA buffers on `hip_stream` (a
  * hipStream_t; NULL = the library's per-thread stream). Asynchronous: returns after the
- * launch. Returns 0, or -1 on invalid arguments / HIP failure (see bhrt_last_error). */
+ * launch. The library's stream is non-blocking: it is NOT ordered after work the caller queued
+ * on the legacy default stream or its own streams (e.g. a hipMemset or a torch fill of the
+ * output arrays) -- synchronize that work first, or pass the stream it runs on. Returns 0, or
+ * -1 on invalid arguments / HIP failure (see bhrt_last_error). */
 int bhrt_render_frame_device(const BlackHoleParams* blackhole, const AccretionDiskParams* disk,
                              const SimulationConfig* config, const bhrt_camera* camera,
                              int width, int height, const bhrt_rows* rows,
