@@ -275,11 +275,13 @@ typedef struct {
 int bhrt_shard_rows(int height, const bhrt_rows* rows);
 
 /* Render (a shard of) a camera frame into DEVICE SoA buffers on `hip_stream` (a
- * hipStream_t; NULL = the library's per-thread stream). Asynchronous: returns after the
- * launch. The library's stream is non-blocking: it is NOT ordered after work the caller queued
- * on the legacy default stream or its own streams (e.g. a hipMemset or a torch fill of the
- * output arrays) -- synchronize that work first, or pass the stream it runs on. Returns 0, or
- * -1 on invalid arguments / HIP failure (see bhrt_last_error). */
+ * hipStream_t). Asynchronous: returns after the launch. hip_stream NULL behaves like a launch
+ * on the legacy default stream: the frame is ordered after all work the caller queued there
+ * (e.g. a hipMemset or a torch fill of the output arrays) and before all work queued there
+ * afterwards (e.g. a hipMemcpy of the results); the kernels run on the library's per-thread
+ * stream, linked to the default stream by two event waits. BHRT_NULL_STREAM=unordered drops
+ * that ordering (the library's stream alone). Returns 0, or -1 on invalid arguments / HIP
+ * failure (see bhrt_last_error). */
 int bhrt_render_frame_device(const BlackHoleParams* blackhole, const AccretionDiskParams* disk,
                              const SimulationConfig* config, const bhrt_camera* camera,
                              int width, int height, const bhrt_rows* rows,
@@ -294,7 +296,8 @@ int bhrt_render_frame_device(const BlackHoleParams* blackhole, const AccretionDi
  * device_out -- device-to-device over xGMI for the peers (peer access enabled on first use),
  * one strided 2-D copy per field and shard. device_out: root-device buffers of width * height
  * elements per field (NULL fields are not produced). Asynchronous on hip_stream (a root-device
- * hipStream_t; NULL = the library's): the frame is complete when that stream's work is. A
+ * hipStream_t): the frame is complete when that stream's work is; NULL = ordered like the
+ * root's legacy default stream, as for bhrt_render_frame_device. A
  * one-shard frame is bhrt_render_frame_device on the root. Replaces the reference's serial
  * per-pixel loop (raytracer.c:795-804 / blackhole_api.c:225-250) on a multi-GPU node. */
 int bhrt_render_frame_gather(const BlackHoleParams* blackhole, const AccretionDiskParams* disk,
@@ -325,7 +328,8 @@ int bhrt_frame_wait(int ticket);
 
 /* Trace n rays already resident on the device (AoS Ray[n]) into DEVICE SoA buffers.
  * method RK4 with disk != NULL is trace_ray; RKF45 with a disk is integrate_photon_path
- * plus trace_ray's disk scan (config C3). */
+ * plus trace_ray's disk scan (config C3). hip_stream as for bhrt_render_frame_device (NULL:
+ * ordered like the legacy default stream). */
 int bhrt_trace_rays_device(const Ray* device_rays, int n, const BlackHoleParams* blackhole,
                            const AccretionDiskParams* disk, const SimulationConfig* config,
                            IntegrationMethod method, int flags,

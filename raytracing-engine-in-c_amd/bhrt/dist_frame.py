@@ -156,8 +156,11 @@ class FramePipeline:
 
     def __init__(self, n, device, world, rank, mode, H, W, row_block=8,
                  fields=abi.SOA_FIELDS, shards=None, gather=RGB_FIELDS, first_shard=0,
-                 slots=2):
+                 slots=2, force_collective=False):
         assert mode in ("shards", "samples")
+        # the collective runs at world > 1; force_collective runs it at world 1 too (a
+        # one-rank process group: the RCCL path exercised on a one-GPU box, tests)
+        self.collective = world > 1 or bool(force_collective)
         self.nslots = max(2, int(slots))  # frames in flight: a slot is reused nslots frames later
         self.world, self.rank, self.mode = world, rank, mode
         self.H, self.W, self.row_block = H, W, row_block
@@ -184,7 +187,7 @@ class FramePipeline:
                 self.colour = [torch.empty(len(self.gather), n, dtype=torch.float64,
                                            device=device) for _ in range(self.nslots)]
             return
-        self.direct = world == 1 and self.shards == 1  # the buffer IS the image
+        self.direct = not self.collective and self.shards == 1  # the buffer IS the image
         if rank == 0 and not self.direct:
             a, b = self.span
             # one [world, bytes] receive tensor per slot; gather writes rank k's range to row k
@@ -197,7 +200,7 @@ class FramePipeline:
         # gloo gathers host tensors only: with device buffers (the one-GPU rehearsal of the
         # N-rank bench, BHRT_BENCH_SHARE_DEVICE) the gathered range travels through host
         # copies; RCCL gathers the device buffers directly
-        self.staged = (world > 1 and torch.device(device).type != "cpu" and
+        self.staged = (self.collective and torch.device(device).type != "cpu" and
                        dist.get_backend() == "gloo")
         if self.staged:
             a, b = self.span
@@ -222,11 +225,11 @@ class FramePipeline:
                 self.works[slot] = dist.reduce(col, dst=0, op=dist.ReduceOp.SUM, async_op=True)
             else:
                 self.works[slot] = True
-        elif self.world > 1 and self.staged:
+        elif self.collective and self.staged:
             self.host_send[slot].copy_(fb.buf[a:b])  # (waits for the render on this stream)
             recv = list(self.host_recv[slot].unbind(0)) if self.rank == 0 else None
             self.works[slot] = dist.gather(self.host_send[slot], recv, dst=0, async_op=True)
-        elif self.world > 1:
+        elif self.collective:
             recv = list(self.gathered[slot].unbind(0)) if self.rank == 0 else None
             self.works[slot] = dist.gather(fb.buf[a:b], recv, dst=0, async_op=True)
         else:

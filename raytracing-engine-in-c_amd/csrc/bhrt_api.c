@@ -92,16 +92,20 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 #define BHRT_MAX_DEV 16
 /* control blocks per context: a launch into a full ring first harvests it, waiting for every
  * launch in flight -- the GPU drains once per BHRT_RING launches of a thread (C3 frames back to
- * back: ~0.3 ms idle per harvest), so the ring is long (256 slots, 2.2 MB per context) */
+ * back: ~0.3 ms idle per harvest), so the ring is long (256 slots of 16.6 KB: 4.26 MB per
+ * context, i.e. per host thread and device) */
 #ifndef BHRT_RING
 #define BHRT_RING 256
 #endif
 #define BHRT_CTL_WORDS 8    /* u64 per control block (64 B)           */
 #define BHRT_QWORDS ((1 << BHRT_MAX_QUEUE_BITS) * BHRT_QUEUE_STRIDE_MAX) /* queue heads per block */
-/* a launch's control block and its ray-queue heads are one region (zeroed by ONE memset per
- * launch): 64 B of counters, padding to 256 B, then the queue heads */
+/* a launch's control block and its ray-queue heads are one region of the ring: 64 B of
+ * counters, padding to 256 B, then the queue heads. The whole ring is zeroed by one fill on the
+ * GPU after each harvest (ring_order), never per launch. */
 #define BHRT_QHEAD_OFF 32 /* u64 words */
 #define BHRT_SLOT_WORDS (BHRT_QHEAD_OFF + BHRT_QWORDS)
+#define BHRT_RING_BYTES ((size_t)BHRT_RING * BHRT_SLOT_WORDS * sizeof(unsigned long long))
+#define BHRT_RING_STREAMS 8 /* streams remembered as ordered after the ring's last fill */
 #define BHRT_MAX_CHUNKS 8   /* host-buffer frames: pipelined chunks per device            */
 #define BHRT_SCRATCH_SLOTS 8
 #define BHRT_FRAME_SLOTS 3  /* host-buffer frames in flight per thread (bhrt_render_frame_async) */
@@ -121,6 +125,19 @@ typedef struct {
     pending_t pend[BHRT_RING];
     int npend, next_slot;
     hipEvent_t evpool[2 * BHRT_RING];
+    /* the ring's zeroing (ring_order): ring_dirty = harvested, not yet zeroed; ring_ev = the
+     * fill's completion on the stream it ran on; ring_ok = streams already ordered after it */
+    int ring_dirty, n_ring_ok;
+    hipEvent_t ring_ev;
+    hipStream_t ring_ok[BHRT_RING_STREAMS];
+    /* harvest's counter read: libbhrt's control stream (created on first use; never the
+     * legacy null stream, which would also wait for the caller's default-stream work) and
+     * pinned staging for the ring's counter words */
+    hipStream_t ctl_st;
+    unsigned long long* h_ctl;
+    /* NULL hip_stream of the device API (null_fence): the caller's default stream -> libbhrt's
+     * stream before the launch, and back after it */
+    hipEvent_t nul_in, nul_out;
     /* growable device buffers */
     void* d_rays;
     size_t cap_rays;
@@ -282,7 +299,6 @@ int bhrt_device_count(void) {
     return n;
 }
 
-static hipError_t ring_zero(devctx_t* c);
 static devctx_t* ctx_get(int device) {
     if (device < 0 || device >= BHRT_MAX_DEV) {
         set_err("device %d out of range", device);
@@ -296,27 +312,33 @@ static devctx_t* ctx_get(int device) {
     devctx_t* c = (devctx_t*)calloc(1, sizeof *c);
     if (!c) return NULL;
     c->device = device;
-    if (hipMalloc((void**)&c->d_ctl,
-                  (size_t)BHRT_RING * BHRT_SLOT_WORDS * sizeof(unsigned long long)) != hipSuccess) {
-        set_err("cannot create HIP stream / control blocks on device %d", device);
+    if (hipMalloc((void**)&c->d_ctl, BHRT_RING_BYTES) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_ctl,
+                      (size_t)BHRT_RING * BHRT_CTL_WORDS * sizeof(unsigned long long), 0) !=
+            hipSuccess) {
+        set_err("cannot allocate the control blocks on device %d", device);
         free(c);
         return NULL;
     }
-    if (ring_zero(c) != hipSuccess) {
-        set_err("cannot zero the control blocks on device %d", device);
-        free(c);
-        return NULL;
-    }
+    c->ring_dirty = 1; /* zeroed on the GPU by the first launch (ring_order) */
     {   /* the harvest's strided D2H copy once here: its first use in a process loads the
          * runtime's copy kernels (~7 ms, measured as GPU idle time before bench.py's timed
          * frames when the first harvest came there) */
-        unsigned long long h[BHRT_CTL_WORDS];
-        if (hipMemcpy2D(h, sizeof h, c->d_ctl, BHRT_SLOT_WORDS * sizeof(unsigned long long),
-                        sizeof h, 1, hipMemcpyDeviceToHost) != hipSuccess) {
+        if (hipMemcpy2D(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+                        BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                        BHRT_CTL_WORDS * sizeof(unsigned long long), 1,
+                        hipMemcpyDeviceToHost) != hipSuccess) {
             set_err("cannot read the control blocks on device %d", device);
             free(c);
             return NULL;
         }
+    }
+    if (hipEventCreateWithFlags(&c->ring_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->nul_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->nul_out, hipEventDisableTiming) != hipSuccess) {
+        set_err("hipEventCreate failed");
+        free(c);
+        return NULL;
     }
     if (hipEventCreate(&c->span_ref) != hipSuccess) {
         set_err("hipEventCreate failed");
@@ -450,38 +472,72 @@ static void* stream_scratch(devctx_t* c, hipStream_t stream, size_t bytes) {
     return c->scratch[slot].p;
 }
 
-/* zero the whole control ring (no launch of this context may be in flight) */
-static hipError_t ring_zero(devctx_t* c) {
-    hipError_t e = hipMemsetAsync(c->d_ctl, 0,
-                                  (size_t)BHRT_RING * BHRT_SLOT_WORDS * sizeof(unsigned long long),
-                                  (hipStream_t)0);
-    return e != hipSuccess ? e : hipStreamSynchronize((hipStream_t)0);
+/* The control ring is zeroed on the GPU, never with a host sync: after a harvest (ring_dirty)
+ * the next launch fills the whole ring on its own stream before its kernel, and a launch on
+ * any other stream in the same cycle first waits for that fill (an event wait; the streams
+ * already ordered after it are remembered). Each launch of a cycle takes a slot no earlier
+ * launch of the cycle used, so the fill is the only ordering a slot needs. (Round 5 zeroed
+ * the ring on the legacy null stream and synchronised it: a host stall behind every piece of
+ * default-stream work of the caller, once per BHRT_RING launches.) */
+static int ring_order(devctx_t* c, hipStream_t st) {
+    if (c->ring_dirty) {
+        HIP_TRY(hipMemsetAsync(c->d_ctl, 0, BHRT_RING_BYTES, st));
+        HIP_TRY(hipEventRecord(c->ring_ev, st));
+        c->ring_dirty = 0;
+        c->ring_ok[0] = st;
+        c->n_ring_ok = 1;
+        return 0;
+    }
+    for (int i = 0; i < c->n_ring_ok; i++)
+        if (c->ring_ok[i] == st) return 0;
+    HIP_TRY(hipStreamWaitEvent(st, c->ring_ev, 0));
+    if (c->n_ring_ok < BHRT_RING_STREAMS) c->ring_ok[c->n_ring_ok++] = st;
+    return 0;
 }
 
-/* fold finished launches into g_stats (waits for them); fold = 0 discards them unread (no
- * counter copy, no event timing: a caller resetting the statistics before a timed region must
- * not leave the GPU idle for the ~0.2 ms per launch that the event queries take, bench.py) */
+/* libbhrt's control stream of a context (device current), created on first use */
+static int own_stream(hipStream_t* s);
+static int ctl_stream(devctx_t* c) {
+    if (c->ctl_st) return 0;
+    if (own_stream(&c->ctl_st)) {
+        c->ctl_st = NULL;
+        set_err("cannot create libbhrt's control stream on device %d", c->device);
+        return -1;
+    }
+    return 0;
+}
+
+/* Wait for the pending launches and read their counters; fold them into g_stats (fold = 0
+ * drops them unread, without the per-launch event timing: a caller resetting the statistics
+ * right before a timed region must not leave the GPU idle for the ~0.2 ms per launch that the
+ * event queries take, bench.py). Either way a launch whose redo pass was left out (the host
+ * proved no ray can need it, origin_no_evict) must not have handed a ray over: if one did, the
+ * proof was wrong for that scene, the ray's outputs hold RAY_ERROR (k_trace), and this
+ * returns -1 with the count in bhrt_last_error. */
 static int harvest(devctx_t* c, int fold) {
     if (c->npend == 0) return 0;
-    unsigned long long h[BHRT_RING * BHRT_CTL_WORDS];
     HIP_TRY(hipSetDevice(c->device));
     for (int i = 0; i < c->npend; i++) HIP_TRY(hipEventSynchronize(c->pend[i].ev1));
-    if (fold)
-        HIP_TRY(hipMemcpy2D(h, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
-                            BHRT_SLOT_WORDS * sizeof(unsigned long long),
-                            BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
-                            hipMemcpyDeviceToHost));
-    /* every launch of the ring has completed: zero it for the next BHRT_RING (launch() itself issues
-     * no memset -- a fill kernel per frame that had to wait for a free wave slot behind the
-     * other frames' persistent kernels; a slot is reused only after it was harvested here) */
-    HIP_TRY(ring_zero(c));
-    for (int i = 0; fold && i < c->npend; i++) {
-        float t0 = 0.f, t1 = 0.f;  /* start and end relative to span_ref (ms) */
+    if (ctl_stream(c)) return -1;
+    HIP_TRY(hipMemcpy2DAsync(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+                             BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                             BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
+                             hipMemcpyDeviceToHost, c->ctl_st));
+    HIP_TRY(hipStreamSynchronize(c->ctl_st));
+    c->ring_dirty = 1; /* every slot is free again: the next launch zeroes the ring */
+    unsigned long long lost = 0;
+    for (int i = 0; i < c->npend; i++) {
+        const unsigned long long* w = c->h_ctl + c->pend[i].slot * BHRT_CTL_WORDS;
+        if (!c->pend[i].redo) lost += w[6];
+        if (!fold) continue;
+        float t0 = 0.f, t1 = 0.f, dt = 0.f; /* start and end relative to span_ref (ms) */
         HIP_TRY(hipEventElapsedTime(&t0, c->span_ref, c->pend[i].ev0));
         HIP_TRY(hipEventElapsedTime(&t1, c->span_ref, c->pend[i].ev1));
+        /* the launch's own duration from its own pair: a difference of two values relative to
+         * span_ref would lose precision as span_ref ages (float ms) */
+        HIP_TRY(hipEventElapsedTime(&dt, c->pend[i].ev0, c->pend[i].ev1));
         if (t0 < c->span_lo) c->span_lo = t0;
         if (t1 > c->span_hi) c->span_hi = t1;
-        const unsigned long long* w = h + c->pend[i].slot * BHRT_CTL_WORDS;
         g_stats.rays += w[1];
         g_stats.iterations += w[2];
         g_stats.stages_full += w[3];
@@ -490,15 +546,23 @@ static int harvest(devctx_t* c, int fold) {
         g_stats.rays_redone += w[6];
         g_stats.redo_launches += (uint64_t)c->pend[i].redo;
         g_stats.launches += 1;
-        g_stats.kernel_ms += t1 - t0;
+        g_stats.kernel_ms += dt;
     }
     c->npend = 0;
+    if (lost) {
+        set_err("%llu ray(s) needed the large-argument redo pass that the host had proved "
+                "unnecessary and left out: their outputs hold RAY_ERROR (BHRT_SKIP_REDO=0 "
+                "always runs the pass)", lost);
+        return -1;
+    }
     return 0;
 }
 
 int bhrt_get_stats(bhrt_stats* out, int reset) {
     int rc = 0;
     double span = 0.0;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
     for (int d = 0; d < BHRT_MAX_DEV; d++) {
         devctx_t* c = g_ctx[d];
         if (!c) continue;
@@ -506,6 +570,7 @@ int bhrt_get_stats(bhrt_stats* out, int reset) {
         if (c->span_on && c->span_hi > c->span_lo) span += c->span_hi - c->span_lo;
         if (reset) c->span_on = 0;
     }
+    if (cur >= 0) (void)hipSetDevice(cur); /* (harvest makes each context's device current) */
     g_stats.span_ms = span;
     if (out) *out = g_stats;
     if (reset) memset(&g_stats, 0, sizeof g_stats);
@@ -753,7 +818,10 @@ static void fill_origin(bhrt_kparams* kp, const Vector3D* origin) {
     k->sp = sp;
     k->s_r0 = sin(r);
     k->c_r0 = cos(r);
-    kp->no_evict = origin_no_evict(&kp->sc, r, th, ph, st, k->st_tiny, m.g_tt, m.g_rr, m.g_thth,
+    /* BHRT_ASSUME_NO_EVICT=1 (tests only): take the proof as given, so that a scene that does
+     * evict shows what a wrong proof would do -- RAY_ERROR outputs and a harvest error */
+    kp->no_evict = env_int("BHRT_ASSUME_NO_EVICT", 0) ||
+                   origin_no_evict(&kp->sc, r, th, ph, st, k->st_tiny, m.g_tt, m.g_rr, m.g_thth,
                                    k->use_approx);
 }
 
@@ -767,6 +835,7 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     /* the redo list follows the initial-state table (one extra field of the allocation) */
     kp->redo = (int*)(kp->init + (size_t)BHRT_INIT_FIELDS * (size_t)kp->n);
     if (c->npend == BHRT_RING && harvest(c, 1) != 0) return -1;
+    if (ring_order(c, stream)) return -1;
     int slot = c->next_slot;
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
     kp->ctl = c->d_ctl + (size_t)slot * BHRT_SLOT_WORDS;
@@ -918,11 +987,48 @@ static int render_frame_device(const BlackHoleParams* bh, const AccretionDiskPar
     return launch(c, &kp, (hipStream_t)stream);
 }
 
+/* A NULL hip_stream in the device API means what it means for a HIP launch: ordered after
+ * every piece of work the caller queued on the legacy default stream (a hipMemset or a torch
+ * fill of the outputs) and before everything queued there afterwards -- while the kernels
+ * still run on libbhrt's own high-priority stream (own_stream: its own hardware queue). Two
+ * event hops per call, no host sync: the default stream -> libbhrt's stream before the launch
+ * (null_fence(c, 0)) and back after it (null_fence(c, 1)). Round 5 launched NULL calls on
+ * libbhrt's non-blocking stream with no ordering at all, and a torch fill still queued behind
+ * the trace kernel overwrote 3.37 M of 4.15 M rays of a frame;
+ * BHRT_NULL_STREAM=unordered keeps that behaviour as an explicit opt-in. */
+static int null_unordered(void) {
+    const char* e = getenv("BHRT_NULL_STREAM");
+    return e && strcmp(e, "unordered") == 0;
+}
+
+static int null_fence(devctx_t* c, int after) {
+    if (after) {
+        HIP_TRY(hipEventRecord(c->nul_out, c->stream));
+        HIP_TRY(hipStreamWaitEvent((hipStream_t)0, c->nul_out, 0));
+    } else {
+        HIP_TRY(hipEventRecord(c->nul_in, (hipStream_t)0));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->nul_in, 0));
+    }
+    return 0;
+}
+
+/* the current device's context with libbhrt's streams, for a NULL-stream call */
+static devctx_t* null_ctx(void) {
+    devctx_t* c = ctx_get(current_device());
+    return c && ctx_streams(c) == 0 ? c : NULL;
+}
+
 int bhrt_render_frame_device(const BlackHoleParams* bh, const AccretionDiskParams* dk,
                              const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
                              const bhrt_rows* rows, IntegrationMethod method, int flags,
                              const bhrt_frame_soa* out, void* stream) {
-    return render_frame_device(bh, dk, cfg, cam, W, H, rows, method, flags, out, stream, 1);
+    if (stream || null_unordered())
+        return render_frame_device(bh, dk, cfg, cam, W, H, rows, method, flags, out, stream, 1);
+    devctx_t* c = null_ctx();
+    if (!c || null_fence(c, 0)) return -1;
+    const int rc =
+        render_frame_device(bh, dk, cfg, cam, W, H, rows, method, flags, out, c->stream, 1);
+    return null_fence(c, 1) ? -1 : rc;
 }
 
 /* origin: non-NULL when the host knows every ray starts at *origin (shared_origin): the
@@ -965,7 +1071,13 @@ int bhrt_trace_rays_device(const Ray* d_rays, int n, const BlackHoleParams* bh,
                            const AccretionDiskParams* dk, const SimulationConfig* cfg,
                            IntegrationMethod method, int flags, const bhrt_frame_soa* out,
                            void* stream) {
-    return trace_rays_device(d_rays, NULL, n, bh, dk, cfg, method, flags, out, stream, NULL);
+    if (stream || null_unordered())
+        return trace_rays_device(d_rays, NULL, n, bh, dk, cfg, method, flags, out, stream, NULL);
+    devctx_t* c = null_ctx(); /* NULL stream: ordered like the legacy default stream */
+    if (!c || null_fence(c, 0)) return -1;
+    const int rc =
+        trace_rays_device(d_rays, NULL, n, bh, dk, cfg, method, flags, out, c->stream, NULL);
+    return null_fence(c, 1) ? -1 : rc;
 }
 
 /* whether rays[0, n) all start at rays[0].origin (bit for bit) */
@@ -1195,6 +1307,11 @@ static int gather_field(char* dst, const char* src, size_t fs, int W, int H, int
     return 0;
 }
 
+static int gather_frame(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                        const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                        IntegrationMethod method, int flags, const bhrt_frame_soa* out, int ndev,
+                        int S, int total, int root, devctx_t* rc, hipStream_t rs);
+
 int bhrt_render_frame_gather(const BlackHoleParams* bh, const AccretionDiskParams* dk,
                              const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
                              IntegrationMethod method, int flags, const bhrt_frame_soa* out,
@@ -1230,6 +1347,21 @@ int bhrt_render_frame_gather(const BlackHoleParams* bh, const AccretionDiskParam
     devctx_t* rc = ctx_get(root);
     if (!rc || (!stream && ctx_streams(rc))) return -1;
     hipStream_t rs = stream ? (hipStream_t)stream : rc->stream;
+    /* NULL stream: the root's work -- the only writes into device_out -- is ordered like the
+     * legacy default stream's (null_fence); the peers render into libbhrt's own buffers */
+    const int fence = !stream && !null_unordered();
+    if (fence && null_fence(rc, 0)) return -1;
+    const int e = gather_frame(bh, dk, cfg, cam, W, H, method, flags, out, ndev, S, total, root,
+                               rc, rs);
+    if (fence && hipSetDevice(root) == hipSuccess && null_fence(rc, 1)) return -1;
+    return e;
+}
+
+static int gather_frame(const BlackHoleParams* bh, const AccretionDiskParams* dk,
+                        const SimulationConfig* cfg, const bhrt_camera* cam, int W, int H,
+                        IntegrationMethod method, int flags, const bhrt_frame_soa* out, int ndev,
+                        int S, int total, int root, devctx_t* rc, hipStream_t rs) {
+    const int B = 8;
     if (S == 1)
         return render_frame_device(bh, dk, cfg, cam, W, H, NULL, method, flags, out, rs, 0);
     const bhrt_frame_soa fields = device_fields(out, (int)method, dk != NULL, bh->spin != 0.0);

@@ -1732,6 +1732,10 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 n.huge = false;
                 n.rays--;
                 kp.redo[atomicAdd(kp.ctl + 6, 1ull)] = rid;
+                // no redo pass follows a launch the host proved eviction-free: if that proof
+                // was wrong for this scene, the ray is marked, never left stale (the host's
+                // harvest reports the count as an error, bhrt_api.c)
+                if (kp.no_evict && kp.skip_redo && kp.out.result) kp.out.result[rid] = RAY_ERROR;
                 live = false;
             } else if (term != T_NONE) {
                 if constexpr (DEFER)

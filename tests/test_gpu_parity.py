@@ -744,6 +744,76 @@ def test_async_frames_in_flight_equal_sync_frames(bhrt_lib):
             assert np.array_equal(arrays[f], want[f], equal_nan=True), (cname, camname, f)
 
 
+def _default_stream_filled_outputs(torch, n):
+    """SoA output tensors of n rays whose fills are still queued on torch's default stream
+    (the legacy null stream) when this returns: a busy kernel first, then a poison fill of
+    every field (ints -7 / floats 1e300 through fill_, the hit point through zero_, a memset),
+    so a render that is not ordered after the default stream finds its outputs overwritten.
+    The caller must not synchronise before rendering."""
+    assert torch.cuda.current_stream().cuda_stream == 0  # (torch's default = the null stream)
+    t = {f: torch.empty(n, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
+                        device="cuda") for f in abi.SOA_FIELDS}
+    torch.cuda.synchronize()  # (allocation done; everything below stays queued)
+    sleep = getattr(torch.cuda, "_sleep", None)
+    if sleep is not None:
+        sleep(20_000_000)
+    else:  # a few ms of GPU work on the default stream instead
+        a = torch.ones(2048, 2048, device="cuda")
+        for _ in range(8):
+            a = a @ a * 1e-3
+    for f, v in t.items():
+        if f in ("hit_x", "hit_y", "hit_z"):
+            v.zero_()
+        else:
+            v.fill_(-7 if f in ("result", "steps") else 1e300)
+    return t
+
+
+def test_null_stream_trace_rays_device_orders_after_default_stream(bhrt_lib, oracle):
+    """bhrt_trace_rays_device(..., NULL): the rays are uploaded and the outputs poison-filled
+    on the default stream, the launch takes hip_stream NULL, the results are read back on the
+    default stream -- no host sync in between. Every ray against the oracle (C5's Kerr a = 0.99
+    RKF45 scene, a 160x90 camera's rays)."""
+    import torch
+    c = configs.CONFIGS["C5"]
+    bh, dk, cfg = c.scene()
+    rays = configs.camera_rays(configs.camera("B"), 160, 90)
+    n = len(rays)
+    want = oracle.trace_rays(rays, bh, dk, cfg, c.method, c.flags)
+    L = bhrt_lib.load()
+    t = _default_stream_filled_outputs(torch, n)
+    d_rays = torch.from_numpy(rays.view(np.uint8)).to("cuda", non_blocking=True)
+    assert L.bhrt_trace_rays_device(d_rays.data_ptr(), n, C.byref(bh), C.byref(dk) if dk else None,
+                                    C.byref(cfg), c.method, c.flags,
+                                    C.byref(bhrt_lib.soa_from_tensors(t)), None) == 0
+    got = {f: v.cpu().numpy() for f, v in t.items()}
+    compare(got, want, RTOL, sky_pinned(c.method), "C5 rays, NULL stream")
+
+
+def test_wrong_no_evict_proof_is_reported(bhrt_lib, monkeypatch):
+    """the redo launch is left out where the host proves that no ray can be evicted
+    (origin_no_evict). If that proof were wrong for a scene, the evicted rays must not keep
+    stale outputs silently: k_trace marks them RAY_ERROR and the next harvest (bhrt_get_stats)
+    fails with the count. Forced here with the test knob BHRT_ASSUME_NO_EVICT on a scene that
+    hands every ray over (M = 1e-3: the far-field bound is unprovable,
+    test_unbounded_far_field_launch_takes_the_redo_path)."""
+    cam = configs.camera("B")
+    dk = abi.disk(0.006, 0.04, 1.0, 1.0)
+    bh = abi.black_hole(1.0e-3, 0.0)
+    cfg = abi.sim_config(0.1, 100.0, 300, 1e-6)
+    bhrt_lib.stats(reset=True)
+    monkeypatch.setenv("BHRT_ASSUME_NO_EVICT", "1")
+    got = bhrt_lib.render_frame(bh, dk, cfg, cam, 40, 24, abi.INTEGRATOR_RK4, 0)
+    assert (got["result"] == abi.RAY_ERROR).all(), np.unique(got["result"])
+    with pytest.raises(bhrt_lib.BhrtError, match="redo pass"):
+        bhrt_lib.stats(reset=True)
+    monkeypatch.delenv("BHRT_ASSUME_NO_EVICT")
+    assert bhrt_lib.stats(reset=True)["launches"] == 0  # (the error is reported once)
+    got = bhrt_lib.render_frame(bh, dk, cfg, cam, 40, 24, abi.INTEGRATOR_RK4, 0)
+    assert not (got["result"] == abi.RAY_ERROR).any()
+    assert bhrt_lib.stats(reset=True)["rays_redone"] == 40 * 24
+
+
 @pytest.mark.parametrize("cname", ["C1", "C2", "C3", "C4", "C5"])
 def test_full_frame_every_ray_vs_oracle(bhrt_lib, oracle, cname):
     """Every ray of the frame bench.py renders at N = 1 (camera B) against the oracle: C1
@@ -759,14 +829,14 @@ def test_full_frame_every_ray_vs_oracle(bhrt_lib, oracle, cname):
     W, H = plan.width, plan.height
     rows = plan.rows(0)
     n = W * (H if rows is None else bhrt_lib.shard_rows(H, rows))
-    t = {f: torch.zeros(n, dtype=torch.int32 if f in ("result", "steps") else torch.float64,
-                        device="cuda") for f in abi.SOA_FIELDS}
-    # torch zero-fills on its stream, libbhrt renders on its own non-blocking one: without this
-    # sync a fill still queued behind the trace kernel's resident waves overwrites its output
-    torch.cuda.synchronize()
+    # The outputs are filled on torch's default stream (the legacy null stream) behind a busy
+    # kernel, rendered with hip_stream NULL and read back on the default stream, with no host
+    # sync anywhere: NULL orders the frame after the fills and before the reads (null_fence,
+    # bhrt_api.c). Round 5 needed a torch.cuda.synchronize() on each side (a fill still queued
+    # behind the trace kernel overwrote 3.37 M rays of C5's frame).
+    t = _default_stream_filled_outputs(torch, n)
     bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags,
-                                 bhrt_lib.soa_from_tensors(t), 0)
-    torch.cuda.synchronize()
+                                 bhrt_lib.soa_from_tensors(t), None)
     got = {f: v.cpu().numpy() for f, v in t.items()}
     del t
     want, margin = oracle.render_frame_margin(bh, dk, cfg, cam, W, H, c.method, c.flags,
