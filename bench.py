@@ -375,7 +375,7 @@ def main():
     torch.cuda.synchronize()
     t_idle = time.perf_counter()  # the GPU is idle from here to the first timed launch
     lib.stats_discard()
-    pipe.collective_ms.clear()
+    pipe.reset_timing()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -388,6 +388,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    pipe.collect_timing()  # (the collectives' own GPU time, read after the sync)
     elapsed_rank = elapsed
     st = lib.stats(reset=True)
     if world > 1:
@@ -534,6 +535,7 @@ def main():
                                      "mean": round(float(np.nanmean(cms)), 4),
                                      "per_rank": [round(float(v), 4) for v in cms]}
                                     if np.isfinite(cms).any() else None),
+            "gather_timing_error": pipe.timing_error,
             "gather": (f"one {dist.get_backend()} gather of the {args.gather} fields to rank 0 "
                        "per frame, overlapped with the next frame; its GPU time from the "
                        "process group's own events (TORCH_NCCL_ENABLE_TIMING; not measured "

@@ -176,8 +176,12 @@ class FramePipeline:
             raise ValueError("samples mode reduces the colour planes only")
         self.works = [None] * self.nslots
         # the collective's own GPU time per completed frame (ms), where the process group
-        # times its work (RCCL with TORCH_NCCL_ENABLE_TIMING=1: Work.get_duration)
+        # times its work (RCCL with TORCH_NCCL_ENABLE_TIMING=1: Work._get_duration), filled by
+        # collect_timing() once the device has synchronised: wait() only orders the current
+        # stream after the collective, and its end event cannot be read before it completes
         self.collective_ms = []
+        self.timing_error = None
+        self._timed = []
         self.frames = 0
         self.last = None
         self.images = self.gathered = self.colour = None
@@ -238,6 +242,24 @@ class FramePipeline:
             self.works[slot] = True
         self.frames += 1
 
+    def collect_timing(self):
+        """Move the GPU time of every collective completed since the last call into
+        collective_ms (call after torch.cuda.synchronize()); unmeasured (gloo, or timing not
+        enabled): collective_ms stays as it was and timing_error says why."""
+        for w in self._timed:
+            try:
+                dur = getattr(w, "get_duration", None) or w._get_duration  # (torch 2.10: _get_duration)
+                self.collective_ms.append(float(dur()))
+            except Exception as e:  # (gloo, or TORCH_NCCL_ENABLE_TIMING unset)
+                self.timing_error = repr(e)[:200]
+        self._timed.clear()
+        return self.collective_ms
+
+    def reset_timing(self):
+        self._timed.clear()
+        self.collective_ms.clear()
+        self.timing_error = None
+
     def finish(self):
         for k in range(max(self.frames - self.nslots, 0), self.frames):  # oldest first
             self._complete(k % self.nslots)
@@ -249,10 +271,7 @@ class FramePipeline:
             return
         if w is not True:
             w.wait()
-            try:
-                self.collective_ms.append(float(w.get_duration()))
-            except Exception:  # (gloo, or timing not enabled: not measured)
-                pass
+            self._timed.append(w)
             if self.staged and self.rank == 0:
                 self.gathered[slot].copy_(self.host_recv[slot])
         self.works[slot] = None

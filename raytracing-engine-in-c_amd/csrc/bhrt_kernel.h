@@ -47,6 +47,8 @@ typedef struct {
     double rot_vmax; /* zero-acceleration paths: a ray with |state[5]| below this turns state[2]
                         by less than pi/4 per step for every step size (geodesic.hip
                         rotation_trig); a ray at or above it is re-traced by the redo pass */
+    int accept_all;  /* RKF45 with 2^-30 <= tol <= 2^300 and finite step sizes: no attempt on the
+                        zero-acceleration paths can be rejected (geodesic.hip rkf45_attempt ACC) */
 } bhrt_scene_k;
 
 typedef struct {

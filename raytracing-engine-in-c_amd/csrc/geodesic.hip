@@ -531,11 +531,33 @@ __device__ __forceinline__ bool rkf45_accept(const double (&err)[6], const doubl
     return tol_normal ? max_error <= tol : max_error / tol <= 1.0;
 }
 
+// Attempts that cannot be rejected (ACC; round 6). Where the stage sums are hoisted (hoist_sums:
+// the zero-acceleration paths, C5) every stage derivative of components 0..2 is the ray's
+// constant v = state[3..5], so s4 = rkf45_sum4(v, v, v, v) and s5 = rkf45_sum5(v, ..., v) are v
+// times weight sums that are exactly 1 in real arithmetic, each within E <= 10u |v| of v (u =
+// 2^-53: <= 5 products and sums, partial sums below 1.5 |v|, the weights' own rounding). The
+// attempt's a = y5 = RN(y + h s5), b = y4 = RN(y + h s4) and err = RN(|a - b|) then satisfy
+//   |a - b| <= |h| |s5 - s4| + u (|a| + |b|)  and  |b| <= |a| + |a - b|,
+// so |a - b| <= (|h| |s5 - s4| + 2u |a|) / (1 - u). And scale = max(|y|, |a|, 1e-10) >= |h v| / 2.1
+// (if |y| < |h v| / 2, then |a| >= |h v| (1 - E) - |y| - u |a|). Hence err / scale <= 2.1 * 2E
+// + 2u (1 + 3u) < 50u < 6e-15 for every component (v = 0: s4 = s5 = 0 and err = 0 exactly;
+// tiny v: the absolute rounding is below 2^-1074 against scale >= 1e-10), whatever the state:
+// every attempt passes the accept test -- RN(max err / scale) / tol <= 1 -- for any
+// tol >= 2^-30 (the host's condition, bhrt_api.c fill_scene: accept_all, with finite step
+// sizes and tol <= 2^300). The attempt is then y <- y5 alone: no y4, error, scale or test, and no
+// fixed point (C5: ~20 of ~87 VALU per attempt). The state is finite there (repair_at_refill),
+// so y + h s5 is too. The redo pass (HUGE) keeps the literal test.
+template <bool SPIN0, bool FAR, bool HUGE>
+constexpr bool accept_all_ok() {
+    return zero_accel<SPIN0, FAR>() && repair_at_refill<INTEGRATOR_RKF45, FAR, HUGE>();
+}
+
 // rkf45_integrate (math_util.c:212-457), n = 6. Returns true on accept (y <- y5).
-template <bool SPIN0, bool FAR, bool HUGE, bool HS = false>
+template <bool SPIN0, bool FAR, bool HUGE, bool HS = false, bool ACC = false>
 __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Scene& sc,
                                               bool far_ok, Counters& n, Trig1& tr,
                                               const double* zs = nullptr) {
+    static_assert(!ACC || (HS && accept_all_ok<SPIN0, FAR, HUGE>()), "ACC: hoisted sums only");
     constexpr double b21 = 1.0 / 4.0;
     constexpr double b31 = 3.0 / 32.0, b32 = 9.0 / 32.0;
     constexpr double b41 = 1932.0 / 2197.0, b42 = -7200.0 / 2197.0, b43 = 7296.0 / 2197.0;
@@ -575,6 +597,11 @@ __device__ __forceinline__ bool rkf45_attempt(double (&y)[6], double h, const Sc
                               : y[i] + h * (b61 * k1[i] + b62 * k2[i] + b63 * k3[i] +
                                             b64 * k4[i] + b65 * k5[i]);
     rhs<SPIN0, FAR, HUGE>(yt, k6, sc, far_ok, n, tr, false);
+    if constexpr (ACC) {  // never rejected (above): y <- y5, the same expression as below
+#pragma unroll
+        for (int i = 0; i < 3; i++) y[i] = y[i] + h * zs[3 + i];
+        return true;
+    }
     double y5[6];
     // :367-391 and :402-434 (rkf45_accept)
     constexpr bool FAST_NORM = repair_at_refill<INTEGRATOR_RKF45, FAR, HUGE>();
@@ -933,7 +960,7 @@ constexpr bool hcache() {
 // One pass of integrate_photon_path's loop body (raytracer.c:517-665) plus, with DISK, the
 // on-the-fly form of trace_ray's segment scan. Returns the termination, or T_NONE.
 // hs: the step sizes in registers (k_trace), or NULL to read them from the scene.
-template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE>
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, bool ACC = false>
 __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n,
                                            const HSel hs) {
     Counters* const hc = HUGE ? nullptr : &n;
@@ -999,7 +1026,7 @@ __device__ __forceinline__ int ray_iterate(Ray_& R, const Scene& sc, Counters& n
     if (METHOD == INTEGRATOR_RK4) {
         rk4_step<SPIN0, FAR, HUGE, HS>(R.y, h, sc, R.far_ok, n, tr, R.zs);
     } else if (METHOD == INTEGRATOR_RKF45) {
-        moved = rkf45_attempt<SPIN0, FAR, HUGE, HS>(R.y, h, sc, R.far_ok, n, tr, R.zs);
+        moved = rkf45_attempt<SPIN0, FAR, HUGE, HS, ACC>(R.y, h, sc, R.far_ok, n, tr, R.zs);
     } else {
         moved = false;  // LEAPFROG / YOSHIDA: "not implemented", state unchanged (:616-624)
     }
@@ -1478,7 +1505,7 @@ constexpr int unroll_n() {
 // a = 0 RK4 disk path; ray arrays from trace_rays_batch take 2, so a chunk's
 // trace depends on its upload alone (no set-up kernel queued behind the previous chunk's).
 // The sin/cos anchors of the shared origin are the same for every ray: computed once per wave.
-template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, int INL = 0>
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, int INL = 0, bool ACC = false>
 __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const unsigned long long total =
         HUGE ? *(volatile unsigned long long*)(kp.ctl + 6) : (unsigned long long)kp.n;
@@ -1706,7 +1733,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
         st_trips++;
 #endif
         if (live) {
-            int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, hsel);
+            int term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE, ACC>(R, kp.sc, n, hsel);
             // further iterations in the same trip for rays that go on: the loop's hand-over
             // copies between iterations (state, point, distance, carried sin/cos) fold away. A
             // lane's iterations are the same either way; only its refill point moves.
@@ -1718,13 +1745,13 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
 #pragma unroll
             for (int u = 1; u < unroll_n<METHOD, SPIN0, HUGE>(); u++) {
                 if (__ballot(term != T_NONE || n.huge) != 0ull) break;
-                term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, hsel);
+                term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE, ACC>(R, kp.sc, n, hsel);
             }
 #else
 #pragma unroll
             for (int u = 1; u < unroll_n<METHOD, SPIN0, HUGE>(); u++)
                 if (term == T_NONE && !n.huge)
-                    term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE>(R, kp.sc, n, hsel);
+                    term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE, ACC>(R, kp.sc, n, hsel);
 #endif
             if (METHOD == INTEGRATOR_RK4 && (term != T_NONE || (!HUGE && n.huge)))
                 n.iters += R.k;  // every RK4 iteration moves, so R.k = iterations executed
@@ -1916,7 +1943,7 @@ int claim_shift(int blocks, int claim_div, int queue_bits, int lanes = 256) {
     return shift;
 }
 
-template <int METHOD, bool DISK, bool SPIN0, bool FAR, int INL>
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, int INL, bool ACC = false>
 void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     // resident workgroups of the two instantiations, per device (and per hot block size:
     // kp.block_lanes, 64/128/256 lanes -- a workgroup's slot frees only once ALL its waves
@@ -1929,7 +1956,7 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     int cap_huge = grid_huge[dev].load(std::memory_order_relaxed);
     if (cap == 0 || cap_huge == 0) {
         cap = resident_blocks(
-            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, false, INL>), dev,
+            reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, false, INL, ACC>), dev,
             lanes);
         cap_huge = resident_blocks(
             reinterpret_cast<const void*>(&k_trace<METHOD, DISK, SPIN0, FAR, true, INL>), dev);
@@ -1963,7 +1990,7 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     if (blocks < 1) blocks = 1;
     bhrt_kparams k = kp;
     k.claim_shift = claim_shift(blocks, kp.claim_div, kp.queue_bits, lanes);
-    k_trace<METHOD, DISK, SPIN0, FAR, false, INL><<<blocks, lanes, 0, st>>>(k);
+    k_trace<METHOD, DISK, SPIN0, FAR, false, INL, ACC><<<blocks, lanes, 0, st>>>(k);
     // A launch the host proved eviction-free (bhrt_api.c origin_no_evict: every ray starts at
     // one origin, and every state the loop can reach keeps its sincos arguments below 2^20 --
     // C1, C2, C3 -- or, on the zero-acceleration paths, C4 and C5, the loop has no sincos and
@@ -2007,7 +2034,23 @@ int launch_t(const bhrt_kparams& kp, hipStream_t st, hipEvent_t ev0, hipEvent_t 
         k_init<BHRT_SRC_RAYS><<<grid_for(reinterpret_cast<const void*>(&k_init<BHRT_SRC_RAYS>),
                                          kp.n), 256, 0, st>>>(kp);
     if (ev0) (void)hipEventRecord(ev0, st);
-    if constexpr (CAN_INL) {
+    // attempts that cannot be rejected (rkf45_attempt ACC): the zero-acceleration RKF45
+    // instantiations with the host's accept_all (C5)
+    constexpr bool CAN_ACC = METHOD == INTEGRATOR_RKF45 && accept_all_ok<SPIN0, FAR, false>();
+    if constexpr (CAN_ACC && CAN_INL) {
+        if (kp.sc.accept_all && inl == 1)
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, 1, true>(kp, st);
+        else if (kp.sc.accept_all && inl == 2)
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, 2, true>(kp, st);
+        else if (kp.sc.accept_all)
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, 0, true>(kp, st);
+        else if (inl == 1)
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, 1>(kp, st);
+        else if (inl == 2)
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, 2>(kp, st);
+        else
+            launch_trace_pair<METHOD, DISK, SPIN0, FAR, 0>(kp, st);
+    } else if constexpr (CAN_INL) {
         if (inl == 1)
             launch_trace_pair<METHOD, DISK, SPIN0, FAR, 1>(kp, st);
         else if (inl == 2)

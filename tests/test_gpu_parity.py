@@ -790,6 +790,27 @@ def test_null_stream_trace_rays_device_orders_after_default_stream(bhrt_lib, ora
     compare(got, want, RTOL, sky_pinned(c.method), "C5 rays, NULL stream")
 
 
+@pytest.mark.parametrize("tol", [1e-8, 2.0**-30, 1e-12])
+def test_accept_all_attempts_equal_the_tested_ones(bhrt_lib, oracle, monkeypatch, tol):
+    """rkf45_attempt ACC (geodesic.hip): on the zero-acceleration RKF45 paths an attempt's error
+    is rounding alone, so for tol >= 2^-30 the host lets every attempt through without the
+    accept test. The frame must be bit-identical to the one that runs the test
+    (BHRT_ACCEPT_ALL=0) and equal the oracle; below 2^-30 (1e-12) the test runs either way.
+    C5's scene (Kerr a = 0.99, RKF45, no disk) on a 192x108 camera-B frame."""
+    c = configs.CONFIGS["C5"]
+    bh, dk, cfg = c.scene()
+    cfg.tolerance = tol
+    cam = configs.camera("B")
+    W, H = 192, 108
+    got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+    monkeypatch.setenv("BHRT_ACCEPT_ALL", "0")
+    tested = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+    for f in abi.SOA_FIELDS:
+        assert np.array_equal(got[f], tested[f], equal_nan=True), f
+    want = oracle.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+    compare(got, want, RTOL, True, f"C5 tol={tol}")
+
+
 def test_wrong_no_evict_proof_is_reported(bhrt_lib, monkeypatch):
     """the redo launch is left out where the host proves that no ray can be evicted
     (origin_no_evict). If that proof were wrong for a scene, the evicted rays must not keep

@@ -55,7 +55,8 @@ def test_rccl_gather_of_a_c4_shard_at_world_one(bhrt_lib, monkeypatch):
                 pipe.submit()
         frame = pipe.finish()
         torch.cuda.synchronize()
-        assert len(pipe.collective_ms) == frames
+        pipe.collect_timing()
+        assert len(pipe.collective_ms) == frames, pipe.timing_error
         assert all(np.isfinite(v) and v > 0 for v in pipe.collective_ms), pipe.collective_ms
         # the one-launch frame's display buffer (C4 writes rgba8 from the trace kernel)
         full = torch.zeros((W * H, 4), dtype=torch.uint8, device=dev)

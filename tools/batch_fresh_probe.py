@@ -12,6 +12,7 @@ calls, then the mode's action, then more calls; per call the wall ms. Modes:
   rays_dev     64 rays through bhrt_trace_rays_device (NULL stream) instead of a frame
   batch_small  a 64-ray trace_rays_batch instead
   env:K=V,...  base with extra environment (e.g. env:BHRT_STREAM_QUEUE=0)
+  MODE@K=V,... a mode with extra environment (e.g. batch_small@BHRT_BATCH_LATE_D2H=0)
 """
 import os
 import subprocess
@@ -80,7 +81,12 @@ def main():
     for m in modes:
         env = dict(os.environ)
         name = m
-        if m.startswith("env:"):
+        if "@" in m:  # mode@K=V,...: a mode with extra environment
+            m, kvs = m.split("@", 1)
+            for kv in kvs.split(","):
+                k, v = kv.split("=", 1)
+                env[k] = v
+        elif m.startswith("env:"):
             for kv in m[4:].split(","):
                 k, v = kv.split("=", 1)
                 env[k] = v

@@ -2,7 +2,7 @@
 """VGPR / SGPR / scratch / occupancy of every k_trace instantiation (hipcc resource remarks).
 
 usage: python tools/resource_usage.py [extra hipcc -D flags]
-Template arguments are printed as METHOD DISK SPIN0 FAR HUGE INL."""
+Template arguments are printed as METHOD DISK SPIN0 FAR HUGE INL [ACC]."""
 import os, re, subprocess, sys
 
 src = os.path.join(os.path.dirname(__file__), "..", "raytracing-engine-in-c_amd", "csrc")
@@ -20,8 +20,8 @@ for l in out.splitlines():
     if m and cur:
         rows[cur][m.group(1).strip()] = m.group(2)
 for k, v in rows.items():
-    m = re.search(r"k_traceILi(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)EL[bi](\d)E", k)
+    m = re.search(r"k_traceILi(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)EL[bi](\d)E(?:Lb(\d)E)?", k)
     if not m:
         continue
-    print("k_trace<%s>" % ",".join(m.groups()), "VGPR", v.get("VGPRs"), "SGPR", v.get("TotalSGPRs"),
+    print("k_trace<%s>" % ",".join(g for g in m.groups() if g is not None), "VGPR", v.get("VGPRs"), "SGPR", v.get("TotalSGPRs"),
           "scratch", v.get("ScratchSize [bytes/lane]"), "waves", v.get("Occupancy [waves/SIMD]"))
