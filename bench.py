@@ -183,6 +183,7 @@ def parse():
                         "frame in 8 shards, C4 the 3840x2160 image in 8, C5 its 8 shards), so "
                         "every rank's work of an N-GPU run can be timed on one GPU "
                         "(tools/plan_shards.sh)")
+    p.add_argument("--batch-fresh-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--gather", choices=("rgba8", "image", "all"), default="rgba8",
                    help="fields gathered to rank 0 at N > 1: the rgba8 display buffer the "
                         "colour pass writes (4 B/ray, default), the f64 colour planes "
@@ -219,6 +220,8 @@ def flops(st, method):
 
 def main():
     args = parse()
+    if args.batch_fresh_child:
+        return batch_fresh_child(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -237,6 +240,14 @@ def main():
                           "master_port": os.environ.get("MASTER_PORT"),
                           "device": 0 if shared else local}), flush=True)
         return
+    c0 = configs.CONFIGS[args.config]
+    fresh = None
+    if (world == 1 and not args.no_host_path and args.fields == "all" and
+            c0.method == abi.INTEGRATOR_RK4 and c0.frame(1).shards == 1 and args.shard is None and
+            args.plan_gpus is None):
+        # the drop-in batch API as the FIRST GPU work of a fresh process,
+        # started before this process touches the GPU
+        fresh = batch_fresh_rate(args)
     dev_index = 0 if shared else local
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
@@ -297,6 +308,10 @@ def main():
                [torch.cuda.Stream(device) for _ in range(4 if auto else nstreams)])
     active = [nstreams]
     frame_no = [0]
+    # per-frame completion latency of the timed frames: a timing event on the frame's stream
+    # right before its render and one right after it (trace kernel + colour pass: the frame's
+    # SoA and display buffer are complete), pre-created so that the timed loop only records
+    lat_pool, lat_used = [], [0]
 
     def step():
         # Frame k renders on streams[k % S]. A persistent k_trace launch ends with a tail in
@@ -306,10 +321,16 @@ def main():
         # same stream.
         s = streams[frame_no[0] % active[0]]
         frame_no[0] += 1
+        ev = lat_pool[lat_used[0]] if lat_used[0] < len(lat_pool) else None
         with torch.cuda.stream(s):
             fb = pipe.next_buffer()
+            if ev:
+                ev[0].record(s)
             lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags, fb.soa(),
                                     s.cuda_stream)
+            if ev:
+                ev[1].record(s)
+                lat_used[0] += 1
             pipe.submit()
 
     # every stream renders at least one untimed frame: a stream's first launch (its hardware
@@ -372,6 +393,8 @@ def main():
             step()
         pipe.finish()
         warmup += sustained
+    lat_pool.extend((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    for _ in range(args.steps))
     torch.cuda.synchronize()
     t_idle = time.perf_counter()  # the GPU is idle from here to the first timed launch
     lib.stats_discard()
@@ -389,6 +412,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     pipe.collect_timing()  # (the collectives' own GPU time, read after the sync)
+    lat_ms = sorted(a.elapsed_time(b) for a, b in lat_pool[:lat_used[0]])
     elapsed_rank = elapsed
     st = lib.stats(reset=True)
     if world > 1:
@@ -493,6 +517,7 @@ def main():
             "sustained_warmup": {"frames": sustained, "ms_asked": WARM_MS,
                                  "idle_before_timed_ms": round((t0 - t_idle) * 1e3, 3)},
             "mean_iterations_per_ray": st["iterations"] / max(st["rays"], 1),
+            "frame_latency_ms": frame_latency(lat_ms, dur_ms),
         },
         "roofline": {
             "bound": "valu-fp64",
@@ -547,12 +572,29 @@ def main():
             args.steps, elapsed / args.steps * 1e3)
     if world == 1 and not args.no_host_path and S == 1:  # (bhrt_render_frame: whole images)
         out["host_path"] = host_path_rate(c, bh, dk, cfg, cam, W, H)
+        if fresh is not None:
+            out["host_path"]["trace_rays_batch_fresh"] = fresh
+            out["host_path"]["trace_rays_batch_fresh_mrays_s"] = fresh.get("mrays_s")
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["max_rel_dhit"], out["class_mismatch"] = cpu_baseline(
             args, c, bh, dk, cfg, cam, frame, H)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def frame_latency(lat_ms, span_ms):
+    """Completion latency of the timed frames: from the timing event recorded on a frame's
+    stream right before its render is enqueued (its stream reached it: the frame's trace can
+    start) to the one right after its colour pass. Against the busy span per frame (the GPU time
+    a frame costs when frames overlap), ratio = median / span."""
+    if not lat_ms:
+        return None
+    med = lat_ms[len(lat_ms) // 2]
+    return {"median": round(med, 4), "p90": round(lat_ms[int(0.9 * (len(lat_ms) - 1))], 4),
+            "max": round(lat_ms[-1], 4), "ratio_to_busy_span": round(med / span_ms, 3),
+            "frames": len(lat_ms),
+            "note": "stream event before the frame's render -> after its colour pass"}
 
 
 def prev_tiles_order(pipe, last, H, W, B, S, shard):
@@ -720,6 +762,51 @@ def host_path_rate(c, bh, dk, cfg, cam, W, H, frames=6):
                     "batch API on the frame's camera rays (RayTraceHit[] out), measured before "
                     "the host-frame legs and again after them; trace_ray = median "
                     "of one drop-in call, PCIe round trip included"}
+
+
+def batch_fresh_rate(args):
+    """trace_rays_batch of the frame's camera rays in a fresh child process whose first GPU work
+    it is (this process has not touched the GPU yet): the first call's wall time (code object
+    load, pinned staging, first-touch) and the rate of the next calls, to compare with
+    host_path.trace_rays_batch_after_frames_mrays_s of this process."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--batch-fresh-child", "--config",
+           args.config, "--camera", args.camera]
+    try:
+        env = dict(os.environ)  # the runtime's own hardware-queue setting, as a C caller has
+        if HWQ_ASKED is None:
+            env.pop("GPU_MAX_HW_QUEUES", None)
+        else:
+            env["GPU_MAX_HW_QUEUES"] = HWQ_ASKED
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # (reported, never fatal: a side leg)
+        return {"error": repr(e)[:300]}
+
+
+def batch_fresh_child(args):
+    import ctypes as C
+    c = configs.CONFIGS[args.config]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera(args.camera)
+    W, H = c.frame(1).width, c.frame(1).height
+    rays = configs.camera_rays(cam, W, H)
+    hits = np.zeros(W * H, dtype=abi.HIT_DTYPE)
+    L = lib.load()
+    bargs = (rays.ctypes.data, W * H, C.byref(bh), C.byref(dk) if dk else None, C.byref(cfg),
+             hits.ctypes.data, 0)
+    ms = []
+    for _ in range(5):
+        t = time.perf_counter()
+        if L.trace_rays_batch(*bargs) != 0:
+            raise RuntimeError(lib.last_error())
+        ms.append((time.perf_counter() - t) * 1e3)
+    later = sorted(ms[1:])
+    med = (later[1] + later[2]) / 2
+    print(json.dumps({"first_call_ms": round(ms[0], 2), "calls_ms": [round(v, 3) for v in ms],
+                      "mrays_s": round(W * H / med / 1e3, 3),
+                      "note": "fresh child process, trace_rays_batch is its first GPU work; "
+                              "mrays_s from the median of calls 2-5"}), flush=True)
 
 
 def pmc_profile(config):

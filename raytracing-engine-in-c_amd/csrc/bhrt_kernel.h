@@ -85,8 +85,12 @@ typedef struct {
  * strong-scaled shard cannot hide). Elsewhere (C2) the separate pass runs on the other
  * stream's tail and costs less than the colour code's registers in the trace loop
  * (profiles/r03_ab/fused_colour_rk4.txt). */
+#ifndef BHRT_FUSE_RK4_SPIN0 /* A/B build switch: 1 = RK4 a = 0 disk scenes (C2) fused too */
+#define BHRT_FUSE_RK4_SPIN0 0
+#endif
 #define BHRT_COLOUR_IN_TRACE(method, has_disk, spin) \
-    ((has_disk) && ((method) == INTEGRATOR_RKF45 || ((method) == INTEGRATOR_RK4 && (spin))))
+    ((has_disk) && ((method) == INTEGRATOR_RKF45 || ((method) == INTEGRATOR_RK4 &&         \
+                                                    ((spin) || BHRT_FUSE_RK4_SPIN0))))
 
 typedef struct {
     bhrt_scene_k sc;
@@ -101,10 +105,11 @@ typedef struct {
     int* redo;            /* [n] ids of rays re-traced with the large-argument path */
     bhrt_camera_k cam;    /* BHRT_SRC_CAMERA                                  */
     bhrt_frame_soa out;   /* device SoA outputs; NULL fields skipped          */
-    unsigned long long* ctl; /* [1..5] counters, [6] redo count, [7] redo queue head;
-                                zeroed per launch */
-    unsigned long long* qhead; /* ray-queue heads, queue q at qhead[q * queue_stride];
-                                  zeroed per launch */
+    unsigned long long* ctl; /* [1..5] counters, [6] redo count, [7] redo queue head; the
+                                launch's slot of the control ring, zero at launch (the ring is
+                                filled with zeros on the GPU after each harvest, bhrt_api.c
+                                ring_order) */
+    unsigned long long* qhead; /* ray-queue heads, queue q at qhead[q * queue_stride]; same slot */
     int queue_bits;       /* 2^queue_bits ray queues (<= BHRT_MAX_QUEUE_BITS)            */
     int queue_stride;     /* u64 words between queue heads (<= BHRT_QUEUE_STRIDE_MAX)     */
     int claim_shift;      /* set by the launcher per launch: a block claim is the queue's
