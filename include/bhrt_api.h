@@ -269,6 +269,12 @@ typedef struct {
                                several streams make this, not kernel_ms, the GPU time     */
     uint64_t redo_launches; /* of those launches, how many were followed by the redo pass
                                (left out where no ray can need it)   */
+    /* per launch, the frame's execution window on the GPU's constant-rate wall clock: its
+     * first trace wave's start to its last store (the trace kernel's last wave, or the separate
+     * colour pass's last workgroup) -- the frame's completion latency once it runs */
+    double   frame_ms;      /* sum over the timed launches                               */
+    double   frame_ms_max;  /* the longest                                               */
+    uint64_t frames_timed;  /* launches with a window (0 where the clock rate is unknown) */
 } bhrt_stats;
 
 /* Number of rows of an image of `height` rows owned by shard rows->shard. */

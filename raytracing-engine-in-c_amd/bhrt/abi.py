@@ -117,7 +117,8 @@ class Stats(C.Structure):
                 ("stages_far", C.c_uint64), ("stages_kerr", C.c_uint64),
                 ("launches", C.c_uint64), ("kernel_ms", C.c_double),
                 ("rays_redone", C.c_uint64), ("span_ms", C.c_double),
-                ("redo_launches", C.c_uint64)]
+                ("redo_launches", C.c_uint64), ("frame_ms", C.c_double),
+                ("frame_ms_max", C.c_double), ("frames_timed", C.c_uint64)]
 
 
 # numpy view of RayTraceHit (160 B, offsets pinned in include/bhrt_types.h)

@@ -97,7 +97,8 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 #ifndef BHRT_RING
 #define BHRT_RING 256
 #endif
-#define BHRT_CTL_WORDS 8    /* u64 per control block (64 B)           */
+#define BHRT_CTL_WORDS 16   /* u64 per control block (128 B): [1..5] counters, [6..7] redo,
+                               [8..10] the launch's execution window (geodesic.hip k_trace) */
 #define BHRT_QWORDS ((1 << BHRT_MAX_QUEUE_BITS) * BHRT_QUEUE_STRIDE_MAX) /* queue heads per block */
 /* a launch's control block and its ray-queue heads are one region of the ring: 64 B of
  * counters, padding to 256 B, then the queue heads. The whole ring is zeroed by one fill on the
@@ -125,6 +126,7 @@ typedef struct {
     pending_t pend[BHRT_RING];
     int npend, next_slot;
     hipEvent_t evpool[2 * BHRT_RING];
+    double clock_khz; /* the device's wall-clock rate (hipDeviceAttributeWallClockRate), 0: unknown */
     /* the ring's zeroing (ring_order): ring_dirty = harvested, not yet zeroed; ring_ev = the
      * fill's completion on the stream it ran on; ring_ok = streams already ordered after it */
     int ring_dirty, n_ring_ok;
@@ -321,6 +323,12 @@ static devctx_t* ctx_get(int device) {
         return NULL;
     }
     c->ring_dirty = 1; /* zeroed on the GPU by the first launch (ring_order) */
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess &&
+            khz > 0)
+            c->clock_khz = (double)khz;
+    }
     {   /* the harvest's strided D2H copy once here: its first use in a process loads the
          * runtime's copy kernels (~7 ms, measured as GPU idle time before bench.py's timed
          * frames when the first harvest came there) */
@@ -547,6 +555,14 @@ static int harvest(devctx_t* c, int fold) {
         g_stats.redo_launches += (uint64_t)c->pend[i].redo;
         g_stats.launches += 1;
         g_stats.kernel_ms += dt;
+        /* the execution window: earliest wave start (stored complemented) to the latest end */
+        const unsigned long long t_end = w[9] > w[10] ? w[9] : w[10];
+        if (c->clock_khz > 0.0 && w[8] != 0 && t_end >= ~w[8]) {
+            const double ms = (double)(t_end - ~w[8]) / c->clock_khz;
+            g_stats.frame_ms += ms;
+            if (ms > g_stats.frame_ms_max) g_stats.frame_ms_max = ms;
+            g_stats.frames_timed += 1;
+        }
     }
     c->npend = 0;
     if (lost) {

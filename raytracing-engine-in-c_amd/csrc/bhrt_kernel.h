@@ -78,19 +78,21 @@ typedef struct {
                                         (t * tile_stride) mod ntiles at step t (scatter) */
 } bhrt_camera_k;
 
-/* Whether the trace kernel writes a scene's colour outputs at each ray's exit (no separate
- * colour pass re-reading the hits): RKF45 scenes with a disk (C3: rays end after ~2 attempts,
- * so the pass is a large share of the frame; +5% same-box) and, since round 4, RK4 scenes with
- * a disk at spin != 0 (C4: the pass and its dispatch are a fixed cost per frame that a
- * strong-scaled shard cannot hide). Elsewhere (C2) the separate pass runs on the other
- * stream's tail and costs less than the colour code's registers in the trace loop
- * (profiles/r03_ab/fused_colour_rk4.txt). */
-#ifndef BHRT_FUSE_RK4_SPIN0 /* A/B build switch: 1 = RK4 a = 0 disk scenes (C2) fused too */
-#define BHRT_FUSE_RK4_SPIN0 0
+/* Whether the trace kernel writes a scene's colour outputs at each ray's exit, from the state in
+ * registers (no separate colour pass re-reading the hits). Since round 6 every scene: the
+ * separate pass of a frame could only start once the trace kernel's last wave had ended, by
+ * when the next frame's persistent workgroups held every wave slot, so a C2 frame's colour
+ * landed ~1 frame late (k_colour dispatches averaged 5.5 ms), and on the
+ * current kernels fusing costs nothing (C2 284.5 vs 284.6 Mrays/s same box,
+ * profiles/r06/ab_fused_colour.txt; C5 +16%, C1 +9%). Scenes without a disk get the sky / horizon colour
+ * alone (geodesic.hip colour_sky). BHRT_FUSE_ALL=0 builds round 5's rule (disk scenes with
+ * RKF45 or a != 0; C3, C4) and BHRT_FUSE_COLOUR=0 at run time takes the separate pass (A/B). */
+#ifndef BHRT_FUSE_ALL
+#define BHRT_FUSE_ALL 1
 #endif
-#define BHRT_COLOUR_IN_TRACE(method, has_disk, spin) \
-    ((has_disk) && ((method) == INTEGRATOR_RKF45 || ((method) == INTEGRATOR_RK4 &&         \
-                                                    ((spin) || BHRT_FUSE_RK4_SPIN0))))
+#define BHRT_COLOUR_IN_TRACE(method, has_disk, spin)                                        \
+    (BHRT_FUSE_ALL ||                                                                       \
+     ((has_disk) && ((method) == INTEGRATOR_RKF45 || ((method) == INTEGRATOR_RK4 && (spin)))))
 
 typedef struct {
     bhrt_scene_k sc;

@@ -1210,6 +1210,20 @@ __device__ __forceinline__ unsigned to_u8(float v) {
 }
 
 
+// Black for the horizon, the sky gradient of raytracer.c:1150-1157 on the ray direction's y
+// otherwise (every ray of a scene without a disk)
+__device__ __forceinline__ void colour_sky(int res, double dy, double& r, double& g, double& b) {
+#pragma clang fp contract(off)
+    if (res == RAY_HORIZON) {
+        r = g = b = 0.0;
+    } else {
+        const double t = 0.5 * (dy + 1.0);
+        r = (1.0 - t) * 1.0 + t * 0.5;
+        g = (1.0 - t) * 1.0 + t * 0.7;
+        b = (1.0 - t) * 1.0 + t * 1.0;
+    }
+}
+
 // The frame colour contract of one ray: calculate_disk_temperature +
 // temperature_to_rgb (+ apply_relativistic_effects with BHRT_FLAG_DOPPLER) of a disk hit at
 // (hx, hy), black for the horizon, the sky gradient of raytracer.c:1150-1157 on the ray
@@ -1267,13 +1281,8 @@ __device__ __forceinline__ void colour_of(const Scene& sc, int res, double hx, d
             g = clampd(g * beam, 0.0, 1.0);
             b = clampd(b * beam, 0.0, 1.0);
         }
-    } else if (res == RAY_HORIZON) {
-        r = g = b = 0.0;
     } else {
-        const double t = 0.5 * (dy + 1.0);
-        r = (1.0 - t) * 1.0 + t * 0.5;
-        g = (1.0 - t) * 1.0 + t * 0.7;
-        b = (1.0 - t) * 1.0 + t * 1.0;
+        colour_sky(res, dy, r, g, b);
     }
 }
 
@@ -1325,7 +1334,10 @@ __device__ __forceinline__ void store_ray(const bhrt_kparams& kp, int i, const R
     if (kp.colour_fused && (kp.out.rgb_r || kp.out.rgba32f || kp.out.rgba8)) {
         const int res = term == T_DISK ? RAY_DISK : (term == T_HORIZON ? RAY_HORIZON : RAY_MAX_STEPS);
         double r, g, b;
-        colour_of(kp.sc, res, R.px, R.py, R.dx, R.dy, R.dz, r, g, b);
+        if constexpr (DISK)
+            colour_of(kp.sc, res, R.px, R.py, R.dx, R.dy, R.dz, r, g, b);
+        else  // (no disk: no disk colour code in the kernel)
+            colour_sky(res, R.dy, r, g, b);
         store_colour(kp.out, i, r, g, b);
     }
 }
@@ -1446,9 +1458,14 @@ template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, int INL>
 constexpr bool c3_camera() {
     return METHOD == INTEGRATOR_RKF45 && DISK && SPIN0 && !FAR && !HUGE && INL == 1;
 }
-template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, int INL>
+// the accept-all attempts (ACC, C5): BHRT_ACC_WAVES per SIMD
+#ifndef BHRT_ACC_WAVES
+#define BHRT_ACC_WAVES 4
+#endif
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, bool HUGE, int INL, bool ACC = false>
 constexpr int trace_waves_k() {
-    return c3_camera<METHOD, DISK, SPIN0, FAR, HUGE, INL>() ? 3 : trace_waves<METHOD, DISK, SPIN0>();
+    return ACC ? BHRT_ACC_WAVES
+         : c3_camera<METHOD, DISK, SPIN0, FAR, HUGE, INL>() ? 3 : trace_waves<METHOD, DISK, SPIN0>();
 }
 // Waves per SIMD ONE hot launch takes (0: every resident slot). C3 is resident at 3 waves per
 // SIMD (168 VGPRs, no spills) but launches 2 per SIMD's worth: the frames in flight fill the third
@@ -1470,7 +1487,7 @@ __device__ __forceinline__ unsigned queue_size(unsigned ntotal, unsigned qbits, 
     return (((nb >> qbits) + (q < last ? 1u : 0u)) << 6) + (q == last ? (ntotal & 63u) : 0u);
 }  // k_trace launches 256-lane workgroups
 #define BHRT_TRACE_BOUNDS __attribute__((amdgpu_flat_work_group_size(1, 256), \
-                                         amdgpu_waves_per_eu(trace_waves_k<METHOD, DISK, SPIN0, FAR, HUGE, INL>() > 0 ? trace_waves_k<METHOD, DISK, SPIN0, FAR, HUGE, INL>() : 1)))
+                                         amdgpu_waves_per_eu(trace_waves_k<METHOD, DISK, SPIN0, FAR, HUGE, INL, ACC>() > 0 ? trace_waves_k<METHOD, DISK, SPIN0, FAR, HUGE, INL, ACC>() : 1)))
 
 // Diagnostic build only (make DEFS=-DBHRT_WAVE_STAMPS=1, tools/wave_stamps.py): every wave of a
 // hot k_trace launch records, under the launch's control-block slot, its start and end on the
@@ -1514,6 +1531,11 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const double as1 = kp.cam.s_r0, ac1 = kp.cam.c_r0, as2 = kp.cam.st, ac2 = kp.cam.ct,
                  as3 = kp.cam.sp, ac3 = kp.cam.cp;
     const int lane = threadIdx.x & 63;
+    // the launch's execution window on the constant-rate wall clock (bhrt_stats.frame_ms:
+    // first wave's start to the last wave's end, or the colour pass's end): ctl[8] holds the
+    // complement of the earliest start (the slot is zero at launch, so a maximum), ctl[9] the
+    // latest end
+    if (lane == 0) atomicMax(kp.ctl + 8, ~(unsigned long long)wall_clock64());
 #if BHRT_WAVE_STAMPS
     const unsigned long long st_t0 = (unsigned long long)wall_clock64();
     unsigned st_trips = 0, st_refills = 0, st_claims = 0;
@@ -1804,6 +1826,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     }
 #endif
     if (lane == 0) {
+        atomicMax(kp.ctl + 9, (unsigned long long)wall_clock64());
         if (s0) atomicAdd(kp.ctl + 1, s0);
         if (s1) atomicAdd(kp.ctl + 2, s1);
         if (s2) atomicAdd(kp.ctl + 3, s2);
@@ -1835,6 +1858,8 @@ __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
                   res == RAY_DISK ? s.hit_y[i] : 0.0, dx, dy, dz, r, g, b);
         store_colour(s, i, r, g, b);
     }
+    __syncthreads();  // the frame is complete once the last workgroup's stores are (ctl[10])
+    if (threadIdx.x == 0) atomicMax(kp.ctl + 10, (unsigned long long)wall_clock64());
 }
 
 // integrate_photon_path with a recorded path (one ray, one lane). The output hit goes to
