@@ -308,10 +308,6 @@ def main():
                [torch.cuda.Stream(device) for _ in range(4 if auto else nstreams)])
     active = [nstreams]
     frame_no = [0]
-    # per-frame completion latency of the timed frames: a timing event on the frame's stream
-    # right before its render and one right after it (trace kernel + colour pass: the frame's
-    # SoA and display buffer are complete), pre-created so that the timed loop only records
-    lat_pool, lat_used = [], [0]
 
     def step():
         # Frame k renders on streams[k % S]. A persistent k_trace launch ends with a tail in
@@ -321,16 +317,10 @@ def main():
         # same stream.
         s = streams[frame_no[0] % active[0]]
         frame_no[0] += 1
-        ev = lat_pool[lat_used[0]] if lat_used[0] < len(lat_pool) else None
         with torch.cuda.stream(s):
             fb = pipe.next_buffer()
-            if ev:
-                ev[0].record(s)
             lib.render_frame_device(bh, dk, cfg, cam, W, H, rows, c.method, c.flags, fb.soa(),
                                     s.cuda_stream)
-            if ev:
-                ev[1].record(s)
-                lat_used[0] += 1
             pipe.submit()
 
     # every stream renders at least one untimed frame: a stream's first launch (its hardware
@@ -393,8 +383,6 @@ def main():
             step()
         pipe.finish()
         warmup += sustained
-    lat_pool.extend((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                    for _ in range(args.steps))
     torch.cuda.synchronize()
     t_idle = time.perf_counter()  # the GPU is idle from here to the first timed launch
     lib.stats_discard()
@@ -412,7 +400,6 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     pipe.collect_timing()  # (the collectives' own GPU time, read after the sync)
-    lat_ms = sorted(a.elapsed_time(b) for a, b in lat_pool[:lat_used[0]])
     elapsed_rank = elapsed
     st = lib.stats(reset=True)
     if world > 1:
@@ -517,7 +504,7 @@ def main():
             "sustained_warmup": {"frames": sustained, "ms_asked": WARM_MS,
                                  "idle_before_timed_ms": round((t0 - t_idle) * 1e3, 3)},
             "mean_iterations_per_ray": st["iterations"] / max(st["rays"], 1),
-            "frame_latency_ms": frame_latency(st, lat_ms, dur_ms),
+            "frame_latency_ms": frame_latency(st, dur_ms),
         },
         "roofline": {
             "bound": "valu-fp64",
@@ -583,14 +570,13 @@ def main():
         dist.destroy_process_group()
 
 
-def frame_latency(st, lat_ms, span_ms):
+def frame_latency(st, span_ms):
     """Completion latency of the timed frames. `mean` / `max`: each frame's
     execution window on the GPU's wall clock, stamped by the kernels themselves (bhrt_stats
     frame_ms: the first trace wave's start to the frame's last store -- the trace kernel's last
     wave, or a separate colour pass's last workgroup), against the busy span per frame (the GPU
-    time a frame costs when frames overlap): ratio = mean / span. `queued_to_done`: from a timing
-    event on the frame's stream right before its render to one right after it, i.e. including
-    the wait for the previous frames in flight to free the CUs (two frames deep: ~2 spans)."""
+    time a frame costs when frames overlap): ratio = mean / span. (From enqueue to done a frame
+    also waits for the frames in flight ahead of it to free the CUs: two deep, ~2 spans.)"""
     if not st.get("frames_timed"):
         return None
     mean = st["frame_ms"] / st["frames_timed"]
@@ -598,8 +584,6 @@ def frame_latency(st, lat_ms, span_ms):
            "ratio_to_busy_span": round(mean / span_ms, 3), "frames": st["frames_timed"],
            "note": "kernel-stamped execution window per frame: first trace wave start -> "
                    "last store (colour included)"}
-    if lat_ms:
-        out["queued_to_done_median"] = round(lat_ms[len(lat_ms) // 2], 4)
     return out
 
 

@@ -301,6 +301,7 @@ int bhrt_device_count(void) {
     return n;
 }
 
+static int ctl_stream(devctx_t* c);
 static devctx_t* ctx_get(int device) {
     if (device < 0 || device >= BHRT_MAX_DEV) {
         set_err("device %d out of range", device);
@@ -329,13 +330,16 @@ static devctx_t* ctx_get(int device) {
             khz > 0)
             c->clock_khz = (double)khz;
     }
-    {   /* the harvest's strided D2H copy once here: its first use in a process loads the
-         * runtime's copy kernels (~7 ms, measured as GPU idle time before bench.py's timed
-         * frames when the first harvest came there) */
-        if (hipMemcpy2D(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
-                        BHRT_SLOT_WORDS * sizeof(unsigned long long),
-                        BHRT_CTL_WORDS * sizeof(unsigned long long), 1,
-                        hipMemcpyDeviceToHost) != hipSuccess) {
+    {   /* the harvest's control stream and its strided D2H copy once here: a process's first
+         * use of either (the stream's hardware queue set up, the runtime's copy kernels loaded)
+         * costs ~6-7 ms, measured as GPU idle time before bench.py's timed frames when the
+         * first harvest came there (round 5: the copy; round 6: the new stream, C4 -3%) */
+        if (ctl_stream(c) ||
+            hipMemcpy2DAsync(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+                             BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                             BHRT_CTL_WORDS * sizeof(unsigned long long), 1,
+                             hipMemcpyDeviceToHost, c->ctl_st) != hipSuccess ||
+            hipStreamSynchronize(c->ctl_st) != hipSuccess) {
             set_err("cannot read the control blocks on device %d", device);
             free(c);
             return NULL;

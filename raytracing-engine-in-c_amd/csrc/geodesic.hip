@@ -1319,6 +1319,9 @@ __device__ __forceinline__ void store_colour(const bhrt_frame_soa& s, int i, dou
 #ifndef BHRT_DEFER_STORE
 #define BHRT_DEFER_STORE 1
 #endif
+#ifndef BHRT_FRAME_STAMPS  /* the launch's execution window in ctl[8..10] (bhrt_stats.frame_ms) */
+#define BHRT_FRAME_STAMPS 1
+#endif
 typedef const __attribute__((address_space(4))) bhrt_kparams kparams_as4;
 // (k_trace's only argument: it starts the kernel argument segment)
 __device__ __forceinline__ const bhrt_kparams& cold(const bhrt_kparams&) {
@@ -1533,9 +1536,11 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     const int lane = threadIdx.x & 63;
     // the launch's execution window on the constant-rate wall clock (bhrt_stats.frame_ms:
     // first wave's start to the last wave's end, or the colour pass's end): ctl[8] holds the
-    // complement of the earliest start (the slot is zero at launch, so a maximum), ctl[9] the
-    // latest end
-    if (lane == 0) atomicMax(kp.ctl + 8, ~(unsigned long long)wall_clock64());
+    // complement of the start -- stamped by the first workgroup's first wave alone (workgroups
+    // are dispatched in order; one atomic per wave at the launch's start would serialise 4096
+    // atomics on one word) -- and ctl[9] the latest end
+    if (!HUGE && BHRT_FRAME_STAMPS && blockIdx.x == 0 && threadIdx.x == 0)
+        atomicMax(kp.ctl + 8, ~(unsigned long long)wall_clock64());
 #if BHRT_WAVE_STAMPS
     const unsigned long long st_t0 = (unsigned long long)wall_clock64();
     unsigned st_trips = 0, st_refills = 0, st_claims = 0;
@@ -1784,7 +1789,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
                 // no redo pass follows a launch the host proved eviction-free: if that proof
                 // was wrong for this scene, the ray is marked, never left stale (the host's
                 // harvest reports the count as an error, bhrt_api.c)
-                if (kp.no_evict && kp.skip_redo && kp.out.result) kp.out.result[rid] = RAY_ERROR;
+                if (kc.no_evict && kc.skip_redo && kc.out.result) kc.out.result[rid] = RAY_ERROR;
                 live = false;
             } else if (term != T_NONE) {
                 if constexpr (DEFER)
@@ -1826,7 +1831,7 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
     }
 #endif
     if (lane == 0) {
-        atomicMax(kp.ctl + 9, (unsigned long long)wall_clock64());
+        if (BHRT_FRAME_STAMPS) atomicMax(kp.ctl + 9, (unsigned long long)wall_clock64());
         if (s0) atomicAdd(kp.ctl + 1, s0);
         if (s1) atomicAdd(kp.ctl + 2, s1);
         if (s2) atomicAdd(kp.ctl + 3, s2);
@@ -1858,8 +1863,10 @@ __global__ __launch_bounds__(256) void k_colour(const bhrt_kparams kp) {
                   res == RAY_DISK ? s.hit_y[i] : 0.0, dx, dy, dz, r, g, b);
         store_colour(s, i, r, g, b);
     }
-    __syncthreads();  // the frame is complete once the last workgroup's stores are (ctl[10])
-    if (threadIdx.x == 0) atomicMax(kp.ctl + 10, (unsigned long long)wall_clock64());
+    if (BHRT_FRAME_STAMPS) {
+        __syncthreads();  // the frame is complete once the last workgroup's stores are (ctl[10])
+        if (threadIdx.x == 0) atomicMax(kp.ctl + 10, (unsigned long long)wall_clock64());
+    }
 }
 
 // integrate_photon_path with a recorded path (one ray, one lane). The output hit goes to

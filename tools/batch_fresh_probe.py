@@ -11,6 +11,7 @@ calls, then the mode's action, then more calls; per call the wall ms. Modes:
   frame_hits   the same frame writing only result/steps/hit fields (no colour pass)
   rays_dev     64 rays through bhrt_trace_rays_device (NULL stream) instead of a frame
   batch_small  a 64-ray trace_rays_batch instead
+  warm1        one drop-in trace_ray BEFORE the first batch call (what the first call's cost is)
   env:K=V,...  base with extra environment (e.g. env:BHRT_STREAM_QUEUE=0)
   MODE@K=V,... a mode with extra environment (e.g. batch_small@BHRT_BATCH_LATE_D2H=0)
 """
@@ -46,6 +47,12 @@ def child(mode):
         print(f"  {what:28s} " + " ".join(f"{v:6.2f}" for v in out) +
               f"  ms  (last {W * H / out[-1] / 1e3:6.1f} Mrays/s)", flush=True)
 
+    if mode == "warm1":  # one drop-in trace_ray first: context, code object, streams
+        t = time.perf_counter()
+        hit = abi.RayTraceHit()
+        ray = abi.Ray(cam.position, cam.direction)
+        L.trace_ray(C.byref(ray), C.byref(bh), C.byref(dk), C.byref(cfg), C.byref(hit))
+        print(f"  one trace_ray first: {(time.perf_counter() - t) * 1e3:.2f} ms", flush=True)
     calls("fresh", 4)
     if mode in ("frame", "frame_hits"):
         fields = abi.SOA_FIELDS if mode == "frame" else ("result", "steps", "hit_x", "hit_y",
