@@ -526,10 +526,13 @@ def main():
     out["runtime"] = {
         "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"),
         "hw_queues_set_by_bench": os.environ.get("GPU_MAX_HW_QUEUES") != HWQ_ASKED,
-        "note": "bench.py raises HIP's hardware queues per process to 8 unless "
-                "BHRT_BENCH_HW_QUEUES=default (the box's stock value is 4): with the render "
-                "streams, torch's default stream and RCCL's, 4 queues would put a frame's "
-                "collective behind the next frame's trace kernel"}
+        "note": (f"bench.py set HIP's hardware queues per process to "
+                 f"{os.environ.get('GPU_MAX_HW_QUEUES')} (8, or 16 with more than four render "
+                 "streams) unless BHRT_BENCH_HW_QUEUES=default (the box's stock value is 4): with "
+                 "the render streams, torch's default stream and RCCL's, 4 queues would put a "
+                 "frame's collective behind the next frame's trace kernel"
+                 if os.environ.get("GPU_MAX_HW_QUEUES") != HWQ_ASKED else
+                 "the runtime's own hardware-queue setting (not changed by bench.py)")}
     if per_rank is not None:
         cms = per_rank[:, 3]
         out["dist"] = {
