@@ -203,15 +203,20 @@ def parse():
 # never read and their weighted stage sums are per-ray constants: only what each iteration
 # must form from them is credited -- y + h * sum per component (2 ops; RKF45: y4 and y5, 4),
 # RKF45's error, scale and quotient (7 per component) -- plus the 21 ops outside the
-# components: 27 per RK4 iteration, 54 per RKF45 attempt.
+# components: 27 per RK4 iteration, 54 per RKF45 attempt. An RKF45 attempt that the host proved
+# cannot be rejected (bhrt_stats.attempts_untested, DESIGN.md 2.3: C5) forms no y4, error, scale
+# or quotient: y5 = y + h * sum (2 per component) plus the same 21, 27 like an RK4 iteration.
 ZERO_ACCEL_OPS = {False: 27, True: 54}
+ZERO_ACCEL_UNTESTED_OPS = 27
 
 
 def flops(st, method):
     rkf = method == abi.INTEGRATOR_RKF45
     per_iter = 6 if rkf else 4
     if st["iterations"] > 0 and st["stages_kerr"] == per_iter * st["iterations"]:
-        return ZERO_ACCEL_OPS[rkf] * st["iterations"]
+        untested = st.get("attempts_untested", 0) if rkf else 0
+        return (ZERO_ACCEL_OPS[rkf] * (st["iterations"] - untested) +
+                ZERO_ACCEL_UNTESTED_OPS * untested)
     base, per_live_stage = (194, 29) if rkf else (69, 12)
     live = st["stages_full"] + st["stages_far"]
     return (base * st["iterations"] + per_live_stage * live + 35 * st["stages_full"] +
@@ -305,7 +310,7 @@ def main():
                          fields, shards=S, gather=gather, first_shard=shard - rank,
                          slots=4 if auto else nstreams)
     streams = ([torch.cuda.current_stream()] if nstreams <= 1 else
-               [torch.cuda.Stream(device) for _ in range(4 if auto else nstreams)])
+               [render_stream(device) for _ in range(4 if auto else nstreams)])
     active = [nstreams]
     frame_no = [0]
 
@@ -571,6 +576,28 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def render_stream(device):
+    """One render stream. BHRT_BENCH_RENDER_STREAMS (A/B): torch (default: torch's stream pool),
+    prio (torch's high-priority pool), cumask (a HIP stream with a full CU mask: a hardware queue
+    of its own)."""
+    mode = os.environ.get("BHRT_BENCH_RENDER_STREAMS", "torch")
+    if mode == "prio":
+        return torch.cuda.Stream(device, priority=-1)
+    if mode == "cumask":
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        cus = torch.cuda.get_device_properties(device).multi_processor_count
+        words = (cus + 31) // 32
+        mask = (ctypes.c_uint32 * words)(*[0xFFFFFFFF] * words)
+        if cus % 32:
+            mask[words - 1] = (1 << (cus % 32)) - 1
+        h = ctypes.c_void_p()
+        if hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), mask) != 0:
+            raise SystemExit("hipExtStreamCreateWithCUMask failed")
+        return torch.cuda.ExternalStream(h.value, device=device)
+    return torch.cuda.Stream(device)
 
 
 def frame_latency(st, span_ms):

@@ -275,6 +275,9 @@ typedef struct {
     double   frame_ms;      /* sum over the timed launches                               */
     double   frame_ms_max;  /* the longest                                               */
     uint64_t frames_timed;  /* launches with a window (0 where the clock rate is unknown) */
+    uint64_t attempts_untested; /* of `iterations`, the RKF45 attempts run without the error
+                               estimate and accept test: launches where the host proved every
+                               attempt passes (zero-acceleration paths)     */
 } bhrt_stats;
 
 /* Number of rows of an image of `height` rows owned by shard rows->shard. */

@@ -118,7 +118,8 @@ class Stats(C.Structure):
                 ("launches", C.c_uint64), ("kernel_ms", C.c_double),
                 ("rays_redone", C.c_uint64), ("span_ms", C.c_double),
                 ("redo_launches", C.c_uint64), ("frame_ms", C.c_double),
-                ("frame_ms_max", C.c_double), ("frames_timed", C.c_uint64)]
+                ("frame_ms_max", C.c_double), ("frames_timed", C.c_uint64),
+                ("attempts_untested", C.c_uint64)]
 
 
 # numpy view of RayTraceHit (160 B, offsets pinned in include/bhrt_types.h)

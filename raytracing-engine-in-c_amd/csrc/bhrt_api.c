@@ -116,6 +116,7 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 typedef struct {
     int slot;
     int redo; /* the redo pass was launched after the hot one */
+    int untested; /* RKF45 attempts without the accept test (bhrt_scene_k.accept_all) */
     hipEvent_t ev0, ev1;
 } pending_t;
 
@@ -132,10 +133,7 @@ typedef struct {
     int ring_dirty, n_ring_ok;
     hipEvent_t ring_ev;
     hipStream_t ring_ok[BHRT_RING_STREAMS];
-    /* harvest's counter read: libbhrt's control stream (created on first use; never the
-     * legacy null stream, which would also wait for the caller's default-stream work) and
-     * pinned staging for the ring's counter words */
-    hipStream_t ctl_st;
+    /* pinned staging for the ring's counter words (harvest) */
     unsigned long long* h_ctl;
     /* NULL hip_stream of the device API (null_fence): the caller's default stream -> libbhrt's
      * stream before the launch, and back after it */
@@ -301,7 +299,6 @@ int bhrt_device_count(void) {
     return n;
 }
 
-static int ctl_stream(devctx_t* c);
 static devctx_t* ctx_get(int device) {
     if (device < 0 || device >= BHRT_MAX_DEV) {
         set_err("device %d out of range", device);
@@ -330,20 +327,18 @@ static devctx_t* ctx_get(int device) {
             khz > 0)
             c->clock_khz = (double)khz;
     }
-    {   /* the harvest's control stream and its strided D2H copy once here: a process's first
-         * use of either (the stream's hardware queue set up, the runtime's copy kernels loaded)
-         * costs ~6-7 ms, measured as GPU idle time before bench.py's timed frames when the
-         * first harvest came there (round 5: the copy; round 6: the new stream, C4 -3%) */
-        if (ctl_stream(c) ||
-            hipMemcpy2DAsync(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
-                             BHRT_SLOT_WORDS * sizeof(unsigned long long),
-                             BHRT_CTL_WORDS * sizeof(unsigned long long), 1,
-                             hipMemcpyDeviceToHost, c->ctl_st) != hipSuccess ||
-            hipStreamSynchronize(c->ctl_st) != hipSuccess) {
-            set_err("cannot read the control blocks on device %d", device);
-            free(c);
-            return NULL;
-        }
+    /* the harvest's strided D2H copy once here, on the legacy default stream as bhrt_get_stats'
+     * harvest does it: a process's first such copy (the runtime's copy kernels loaded, the
+     * default stream's queue set up) costs ~6-7 ms, measured as GPU idle time before bench.py's
+     * timed frames when the first harvest came there. Synchronous: it waits once, at context
+     * creation, for what the caller queued on its default stream. */
+    if (hipMemcpy2D(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+                    BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                    BHRT_CTL_WORDS * sizeof(unsigned long long), 1,
+                    hipMemcpyDeviceToHost) != hipSuccess) {
+        set_err("cannot read the control blocks on device %d", device);
+        free(c);
+        return NULL;
     }
     if (hipEventCreateWithFlags(&c->ring_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->nul_in, hipEventDisableTiming) != hipSuccess ||
@@ -507,35 +502,35 @@ static int ring_order(devctx_t* c, hipStream_t st) {
     return 0;
 }
 
-/* libbhrt's control stream of a context (device current), created on first use */
-static int own_stream(hipStream_t* s);
-static int ctl_stream(devctx_t* c) {
-    if (c->ctl_st) return 0;
-    if (own_stream(&c->ctl_st)) {
-        c->ctl_st = NULL;
-        set_err("cannot create libbhrt's control stream on device %d", c->device);
-        return -1;
-    }
-    return 0;
-}
-
 /* Wait for the pending launches and read their counters; fold them into g_stats (fold = 0
  * drops them unread, without the per-launch event timing: a caller resetting the statistics
  * right before a timed region must not leave the GPU idle for the ~0.2 ms per launch that the
  * event queries take, bench.py). Either way a launch whose redo pass was left out (the host
  * proved no ray can need it, origin_no_evict) must not have handed a ray over: if one did, the
  * proof was wrong for that scene, the ray's outputs hold RAY_ERROR (k_trace), and this
- * returns -1 with the count in bhrt_last_error. */
-static int harvest(devctx_t* c, int fold) {
+ * returns -1 with the count in bhrt_last_error.
+ * The counters are read on `st`: the stream of the launch that found the ring full (its earlier
+ * work precedes that launch anyway, and the caller keeps it alive), or with st = NULL -- a
+ * bhrt_get_stats call, itself a synchronisation point -- a synchronous copy on the legacy
+ * default stream. Round 6 first read them on a control stream of libbhrt's own: one hardware
+ * queue more in the process, created before the caller's render streams had theirs, cost C4's
+ * 8-GPU shard 15% (profiles/r06/ab_control_stream.txt). */
+static int harvest(devctx_t* c, int fold, hipStream_t st) {
     if (c->npend == 0) return 0;
     HIP_TRY(hipSetDevice(c->device));
     for (int i = 0; i < c->npend; i++) HIP_TRY(hipEventSynchronize(c->pend[i].ev1));
-    if (ctl_stream(c)) return -1;
-    HIP_TRY(hipMemcpy2DAsync(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
-                             BHRT_SLOT_WORDS * sizeof(unsigned long long),
-                             BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
-                             hipMemcpyDeviceToHost, c->ctl_st));
-    HIP_TRY(hipStreamSynchronize(c->ctl_st));
+    if (st) {
+        HIP_TRY(hipMemcpy2DAsync(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+                                 BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                                 BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
+                                 hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    } else {
+        HIP_TRY(hipMemcpy2D(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+                            BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                            BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
+                            hipMemcpyDeviceToHost));
+    }
     c->ring_dirty = 1; /* every slot is free again: the next launch zeroes the ring */
     unsigned long long lost = 0;
     for (int i = 0; i < c->npend; i++) {
@@ -552,6 +547,7 @@ static int harvest(devctx_t* c, int fold) {
         if (t1 > c->span_hi) c->span_hi = t1;
         g_stats.rays += w[1];
         g_stats.iterations += w[2];
+        if (c->pend[i].untested) g_stats.attempts_untested += w[2];
         g_stats.stages_full += w[3];
         g_stats.stages_far += w[4];
         g_stats.stages_kerr += w[5];
@@ -586,7 +582,7 @@ int bhrt_get_stats(bhrt_stats* out, int reset) {
     for (int d = 0; d < BHRT_MAX_DEV; d++) {
         devctx_t* c = g_ctx[d];
         if (!c) continue;
-        if (harvest(c, out != NULL || !reset) != 0) rc = -1;
+        if (harvest(c, out != NULL || !reset, NULL) != 0) rc = -1;
         if (c->span_on && c->span_hi > c->span_lo) span += c->span_hi - c->span_lo;
         if (reset) c->span_on = 0;
     }
@@ -860,7 +856,7 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     }
     /* the redo list follows the initial-state table (one extra field of the allocation) */
     kp->redo = (int*)(kp->init + (size_t)BHRT_INIT_FIELDS * (size_t)kp->n);
-    if (c->npend == BHRT_RING && harvest(c, 1) != 0) return -1;
+    if (c->npend == BHRT_RING && harvest(c, 1, stream) != 0) return -1;
     if (ring_order(c, stream)) return -1;
     int slot = c->next_slot;
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
@@ -882,6 +878,7 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     pending_t* p = &c->pend[c->npend];
     p->slot = slot;
     p->redo = !(kp->skip_redo && kp->no_evict);
+    p->untested = bhrt_trace_untested(kp);
     p->ev0 = c->evpool[2 * c->npend];
     p->ev1 = c->evpool[2 * c->npend + 1];
     int e = bhrt_launch_trace(kp, (void*)stream, (void*)p->ev0, (void*)p->ev1);

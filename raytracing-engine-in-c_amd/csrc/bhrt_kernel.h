@@ -158,6 +158,8 @@ int bhrt_launch_particles(Particle* d_particles, int count, const bhrt_particle_
  * bhrt_launch_trace records ev0/ev1 (hipEvent_t, may be NULL) around the trace kernel
  * itself, not the set-up or colour passes. */
 int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0, void* ev1);
+/* 1 if bhrt_launch_trace runs kp's RKF45 attempts without the accept test (bhrt_stats) */
+int bhrt_trace_untested(const bhrt_kparams* kp);
 int bhrt_launch_path(const bhrt_kparams* kp, const double* origin4, const double* dir3,
                      Vector3D* d_path, int max_positions, int* d_num, int num_positions_in,
                      void* stream);

@@ -2148,6 +2148,17 @@ extern "C" int bhrt_launch_trace(const bhrt_kparams* kp, void* stream, void* ev0
     }
 }
 
+// whether bhrt_launch_trace runs this launch's RKF45 attempts without the accept test (the
+// ACC instantiations above: the host's accept_all on a zero-acceleration path), for the
+// statistics' attempts_untested
+extern "C" int bhrt_trace_untested(const bhrt_kparams* kp) {
+    if (kp->sc.method != INTEGRATOR_RKF45 || !kp->sc.accept_all) return 0;
+    const bool far = (kp->src == BHRT_SRC_CAMERA || kp->rays_shared) ? kp->cam.use_approx != 0 : true;
+    if (kp->sc.spin0)
+        return far ? accept_all_ok<true, true, false>() : accept_all_ok<true, false, false>();
+    return far ? accept_all_ok<false, true, false>() : accept_all_ok<false, false, false>();
+}
+
 extern "C" __attribute__((visibility("default"))) int bhrt_check_rkf45_accept(
     const double* d_err, const double* d_scale, const double* d_tol, int n, int* d_out,
     void* stream) {

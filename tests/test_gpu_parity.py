@@ -802,9 +802,15 @@ def test_accept_all_attempts_equal_the_tested_ones(bhrt_lib, oracle, monkeypatch
     cfg.tolerance = tol
     cam = configs.camera("B")
     W, H = 192, 108
+    bhrt_lib.stats(reset=True)
     got = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+    st = bhrt_lib.stats(reset=True)  # (bench.py credits untested attempts 27 ops, not 54)
+    assert st["iterations"] > 0
+    assert st["attempts_untested"] == (st["iterations"] if tol >= 2.0**-30 else 0), st
     monkeypatch.setenv("BHRT_ACCEPT_ALL", "0")
     tested = bhrt_lib.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
+    st = bhrt_lib.stats(reset=True)
+    assert st["iterations"] > 0 and st["attempts_untested"] == 0, st
     for f in abi.SOA_FIELDS:
         assert np.array_equal(got[f], tested[f], equal_nan=True), f
     want = oracle.render_frame(bh, dk, cfg, cam, W, H, c.method, c.flags)
