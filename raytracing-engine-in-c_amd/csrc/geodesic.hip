@@ -1504,11 +1504,22 @@ constexpr int kStampSlots = 64, kStampWaves = 8192, kStampWords = 8;
 __device__ unsigned long long g_stamps[kStampSlots * kStampWaves * kStampWords];
 #endif
 
-// Loop iterations per trip of the persistent loop (the HUGE redo pass keeps one): RK4 6,
-// RKF45 2, from same-box sweeps of 1..8 (profiles/r02_ab_unroll.txt).
-template <int METHOD, bool SPIN0, bool HUGE>
+// Loop iterations per trip of the persistent loop (the HUGE redo pass keeps one): RKF45 with the
+// accept test 2, from same-box sweeps of 1..8 (round 2); RK4 a = 0 10 (C2 +0.3…0.5%, C1 +0.5…1%
+// against round 2's 6, same-box; 12 and 16 no better, profiles/r06/ab_unroll.txt). The zero-acceleration
+// paths' short iterations -- C4's RK4 step (~80 VALU) and C5's untested attempt (ACC, ~55) --
+// pay the trip's own cost (the live ballot, the refill test and its scalar loads) for fewer
+// instructions each: 16 per trip, C4 +2.2%, C5 +14.5% same-box against 6 / 2; the sweeps
+// flatten from 12 (C5) / 16 (C4) up to 24 / 32 (profiles/r06/ab_unroll.txt).
+#ifndef BHRT_UNROLL_ZA
+#define BHRT_UNROLL_ZA 16
+#endif
+template <int METHOD, bool SPIN0, bool FAR, bool HUGE, bool ACC = false>
 constexpr int unroll_n() {
-    return HUGE ? 1 : (METHOD == INTEGRATOR_RK4 ? 6 : 2);
+    return HUGE                      ? 1
+         : METHOD == INTEGRATOR_RK4  ? (zero_accel<SPIN0, FAR>() ? BHRT_UNROLL_ZA : 10)
+         : ACC                       ? BHRT_UNROLL_ZA
+                                     : 2;
 }
 
 // Persistent trace kernel: grid = what is resident; each wave refills idle lanes from the
@@ -1770,13 +1781,13 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             // copies of the values a lane that stopped must keep (they are copied once, on the
             // trip's exit edge, instead of after every iteration)
 #pragma unroll
-            for (int u = 1; u < unroll_n<METHOD, SPIN0, HUGE>(); u++) {
+            for (int u = 1; u < unroll_n<METHOD, SPIN0, FAR, HUGE, ACC>(); u++) {
                 if (__ballot(term != T_NONE || n.huge) != 0ull) break;
                 term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE, ACC>(R, kp.sc, n, hsel);
             }
 #else
 #pragma unroll
-            for (int u = 1; u < unroll_n<METHOD, SPIN0, HUGE>(); u++)
+            for (int u = 1; u < unroll_n<METHOD, SPIN0, FAR, HUGE, ACC>(); u++)
                 if (term == T_NONE && !n.huge)
                     term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE, ACC>(R, kp.sc, n, hsel);
 #endif
