@@ -1313,8 +1313,8 @@ __device__ __forceinline__ void store_colour(const bhrt_frame_soa& s, int i, dou
 #ifndef BHRT_COLD_KP
 #define BHRT_COLD_KP 1
 #endif
-#ifndef BHRT_UNIFORM_TRIP
-#define BHRT_UNIFORM_TRIP 0
+#ifndef BHRT_UNIFORM_TRIP  /* 1: every instantiation; 0: none; default: RK4 a = 0 (uniform_trip) */
+#define BHRT_UNIFORM_TRIP 2
 #endif
 #ifndef BHRT_DEFER_STORE
 #define BHRT_DEFER_STORE 1
@@ -1505,8 +1505,9 @@ __device__ unsigned long long g_stamps[kStampSlots * kStampWaves * kStampWords];
 #endif
 
 // Loop iterations per trip of the persistent loop (the HUGE redo pass keeps one): RKF45 with the
-// accept test 2, from same-box sweeps of 1..8 (round 2); RK4 a = 0 10 (C2 +0.3…0.5%, C1 +0.5…1%
-// against round 2's 6, same-box; 12 and 16 no better, profiles/r06/ab_unroll.txt). The zero-acceleration
+// accept test 2, from same-box sweeps of 1..8 (round 2); RK4 a = 0 8 under a wave-uniform guard
+// (uniform_trip; predicated, 10 measured C2 +0.3…0.5%, C1 +0.5…1% against round 2's 6 and 12 / 16
+// no better, profiles/r06/ab_unroll.txt). The zero-acceleration
 // paths' short iterations -- C4's RK4 step (~80 VALU) and C5's untested attempt (ACC, ~55) --
 // pay the trip's own cost (the live ballot, the refill test and its scalar loads) for fewer
 // instructions each: 16 per trip, C4 +2.2%, C5 +14.5% same-box against 6 / 2; the sweeps
@@ -1514,10 +1515,23 @@ __device__ unsigned long long g_stamps[kStampSlots * kStampWaves * kStampWords];
 #ifndef BHRT_UNROLL_ZA
 #define BHRT_UNROLL_ZA 16
 #endif
+#ifndef BHRT_UNROLL_A0
+#define BHRT_UNROLL_A0 8
+#endif
+// The trip's later iterations under a wave-uniform guard (k_trace): RK4 a = 0 (C1, C2), whose
+// predicated form copies ~12 carried values (v_mov_b64) at the end of every iteration for the
+// lanes that stopped; 8 per trip (10 spill: 416 B scratch, C2 -65%). C1 +1.2%, C2 +0.4% against
+// the predicated 10 same-box; the zero-acceleration paths stay predicated (uniform: C4 -1%, C5
+// +-0; profiles/r06/ab_unroll.txt).
+template <int METHOD, bool SPIN0>
+constexpr bool uniform_trip() {
+    return BHRT_UNIFORM_TRIP == 1 ||
+           (BHRT_UNIFORM_TRIP == 2 && METHOD == INTEGRATOR_RK4 && SPIN0);
+}
 template <int METHOD, bool SPIN0, bool FAR, bool HUGE, bool ACC = false>
 constexpr int unroll_n() {
     return HUGE                      ? 1
-         : METHOD == INTEGRATOR_RK4  ? (zero_accel<SPIN0, FAR>() ? BHRT_UNROLL_ZA : 10)
+         : METHOD == INTEGRATOR_RK4  ? (zero_accel<SPIN0, FAR>() ? BHRT_UNROLL_ZA : BHRT_UNROLL_A0)
          : ACC                       ? BHRT_UNROLL_ZA
                                      : 2;
 }
@@ -1775,22 +1789,22 @@ __global__ BHRT_TRACE_BOUNDS void k_trace(const bhrt_kparams kp) {
             // further iterations in the same trip for rays that go on: the loop's hand-over
             // copies between iterations (state, point, distance, carried sin/cos) fold away. A
             // lane's iterations are the same either way; only its refill point moves.
-#if BHRT_UNIFORM_TRIP
-            // wave-uniform guard: the trip goes on only while EVERY live lane does, so the next
-            // iteration runs on the same exec mask -- no per-lane region around it, and no
-            // copies of the values a lane that stopped must keep (they are copied once, on the
-            // trip's exit edge, instead of after every iteration)
+            if constexpr (uniform_trip<METHOD, SPIN0>()) {
+                // wave-uniform guard: the trip goes on only while EVERY live lane does, so the
+                // next iteration runs on the same exec mask -- no per-lane region around it, and
+                // no copies of the values a lane that stopped must keep (they are copied once, on
+                // the trip's exit edge, instead of after every iteration)
 #pragma unroll
-            for (int u = 1; u < unroll_n<METHOD, SPIN0, FAR, HUGE, ACC>(); u++) {
-                if (__ballot(term != T_NONE || n.huge) != 0ull) break;
-                term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE, ACC>(R, kp.sc, n, hsel);
-            }
-#else
-#pragma unroll
-            for (int u = 1; u < unroll_n<METHOD, SPIN0, FAR, HUGE, ACC>(); u++)
-                if (term == T_NONE && !n.huge)
+                for (int u = 1; u < unroll_n<METHOD, SPIN0, FAR, HUGE, ACC>(); u++) {
+                    if (__ballot(term != T_NONE || n.huge) != 0ull) break;
                     term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE, ACC>(R, kp.sc, n, hsel);
-#endif
+                }
+            } else {
+#pragma unroll
+                for (int u = 1; u < unroll_n<METHOD, SPIN0, FAR, HUGE, ACC>(); u++)
+                    if (term == T_NONE && !n.huge)
+                        term = ray_iterate<METHOD, DISK, SPIN0, FAR, HUGE, ACC>(R, kp.sc, n, hsel);
+            }
             if (METHOD == INTEGRATOR_RK4 && (term != T_NONE || (!HUGE && n.huge)))
                 n.iters += R.k;  // every RK4 iteration moves, so R.k = iterations executed
             if (!HUGE && n.huge) {  // hand the ray to the HUGE instantiation
