@@ -90,10 +90,11 @@ double clamp(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi
 /* device contexts                                                                          */
 /* ======================================================================================= */
 #define BHRT_MAX_DEV 16
-/* control blocks per context: a launch into a full ring first harvests it, waiting for every
- * launch in flight -- the GPU drains once per BHRT_RING launches of a thread (C3 frames back to
- * back: ~0.3 ms idle per harvest), so the ring is long (256 slots of 16.6 KB: 4.26 MB per
- * context, i.e. per host thread and device) */
+/* control blocks per context: a launch into a full ring first harvests its older half (the
+ * launches BHRT_RING / 2 and more back, long finished when frames are in flight: the newer half
+ * keeps the GPU busy meanwhile; harvesting every launch drained the GPU once per BHRT_RING
+ * launches, C4 8-GPU shard -1.2%, profiles/r06/ab_half_harvest.txt). 256 slots of 16.6 KB:
+ * 4.26 MB per context, i.e. per host thread and device */
 #ifndef BHRT_RING
 #define BHRT_RING 256
 #endif
@@ -131,6 +132,7 @@ typedef struct {
     /* the ring's zeroing (ring_order): ring_dirty = harvested, not yet zeroed; ring_ev = the
      * fill's completion on the stream it ran on; ring_ok = streams already ordered after it */
     int ring_dirty, n_ring_ok;
+    int dirty_row, dirty_rows; /* the slots the next fill zeroes (harvest) */
     hipEvent_t ring_ev;
     hipStream_t ring_ok[BHRT_RING_STREAMS];
     /* pinned staging for the ring's counter words (harvest) */
@@ -321,6 +323,8 @@ static devctx_t* ctx_get(int device) {
         return NULL;
     }
     c->ring_dirty = 1; /* zeroed on the GPU by the first launch (ring_order) */
+    c->dirty_row = 0;
+    c->dirty_rows = BHRT_RING;
     {
         int khz = 0;
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess &&
@@ -480,15 +484,17 @@ static void* stream_scratch(devctx_t* c, hipStream_t stream, size_t bytes) {
 }
 
 /* The control ring is zeroed on the GPU, never with a host sync: after a harvest (ring_dirty)
- * the next launch fills the whole ring on its own stream before its kernel, and a launch on
- * any other stream in the same cycle first waits for that fill (an event wait; the streams
- * already ordered after it are remembered). Each launch of a cycle takes a slot no earlier
- * launch of the cycle used, so the fill is the only ordering a slot needs. (Round 5 zeroed
- * the ring on the legacy null stream and synchronised it: a host stall behind every piece of
- * default-stream work of the caller, once per BHRT_RING launches.) */
+ * the next launch fills the harvested slots on its own stream before its kernel, and a launch
+ * on any other stream in the same cycle first waits for that fill (an event wait; the streams
+ * already ordered after it are remembered). Each launch of a cycle takes a slot of the filled
+ * range that no earlier launch of the cycle used, so the fill is the only ordering a slot
+ * needs. (Round 5 zeroed the ring on the legacy null stream and synchronised it: a host stall
+ * behind every piece of default-stream work of the caller, once per BHRT_RING launches.) */
 static int ring_order(devctx_t* c, hipStream_t st) {
     if (c->ring_dirty) {
-        HIP_TRY(hipMemsetAsync(c->d_ctl, 0, BHRT_RING_BYTES, st));
+        HIP_TRY(hipMemsetAsync(c->d_ctl + (size_t)c->dirty_row * BHRT_SLOT_WORDS, 0,
+                               (size_t)c->dirty_rows * BHRT_SLOT_WORDS * sizeof(unsigned long long),
+                               st));
         HIP_TRY(hipEventRecord(c->ring_ev, st));
         c->ring_dirty = 0;
         c->ring_ok[0] = st;
@@ -514,26 +520,46 @@ static int ring_order(devctx_t* c, hipStream_t st) {
  * bhrt_get_stats call, itself a synchronisation point -- a synchronous copy on the legacy
  * default stream. Round 6 first read them on a control stream of libbhrt's own: one hardware
  * queue more in the process, created before the caller's render streams had theirs, cost C4's
- * 8-GPU shard 15% (profiles/r06/ab_control_stream.txt). */
-static int harvest(devctx_t* c, int fold, hipStream_t st) {
-    if (c->npend == 0) return 0;
+ * 8-GPU shard 15% (profiles/r06/ab_control_stream.txt).
+ * `count`: how many of the oldest pending launches. A launch that finds the ring full harvests
+ * its older half only (BHRT_RING / 2 launches, long finished when frames are in flight), so the
+ * GPU keeps the newer half's frames while the host reads; it then reuses the freed half. The
+ * slots of the pending launches are consecutive, the ring alternates halves (a full harvest
+ * restarts it at slot 0), and the older half never wraps. bhrt_get_stats harvests everything. */
+static int harvest(devctx_t* c, int fold, hipStream_t st, int count) {
+    if (count > c->npend) count = c->npend;
+    if (count <= 0) return 0;
     HIP_TRY(hipSetDevice(c->device));
-    for (int i = 0; i < c->npend; i++) HIP_TRY(hipEventSynchronize(c->pend[i].ev1));
+    for (int i = 0; i < count; i++) HIP_TRY(hipEventSynchronize(c->pend[i].ev1));
+    const int full = count == c->npend;
+    const int row = full ? 0 : c->pend[0].slot, rows = full ? BHRT_RING : count;
+    if (row + rows > BHRT_RING) {
+        set_err("internal: control ring range %d+%d", row, rows);
+        return -1;
+    }
     if (st) {
-        HIP_TRY(hipMemcpy2DAsync(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+        HIP_TRY(hipMemcpy2DAsync(c->h_ctl + (size_t)row * BHRT_CTL_WORDS,
+                                 BHRT_CTL_WORDS * sizeof(unsigned long long),
+                                 c->d_ctl + (size_t)row * BHRT_SLOT_WORDS,
                                  BHRT_SLOT_WORDS * sizeof(unsigned long long),
-                                 BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
+                                 BHRT_CTL_WORDS * sizeof(unsigned long long), rows,
                                  hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     } else {
-        HIP_TRY(hipMemcpy2D(c->h_ctl, BHRT_CTL_WORDS * sizeof(unsigned long long), c->d_ctl,
+        HIP_TRY(hipMemcpy2D(c->h_ctl + (size_t)row * BHRT_CTL_WORDS,
+                            BHRT_CTL_WORDS * sizeof(unsigned long long),
+                            c->d_ctl + (size_t)row * BHRT_SLOT_WORDS,
                             BHRT_SLOT_WORDS * sizeof(unsigned long long),
-                            BHRT_CTL_WORDS * sizeof(unsigned long long), BHRT_RING,
+                            BHRT_CTL_WORDS * sizeof(unsigned long long), rows,
                             hipMemcpyDeviceToHost));
     }
-    c->ring_dirty = 1; /* every slot is free again: the next launch zeroes the ring */
+    /* the harvested slots are free again: the next launch zeroes them and takes them first */
+    c->ring_dirty = 1;
+    c->dirty_row = row;
+    c->dirty_rows = rows;
+    if (full) c->next_slot = 0;
     unsigned long long lost = 0;
-    for (int i = 0; i < c->npend; i++) {
+    for (int i = 0; i < count; i++) {
         const unsigned long long* w = c->h_ctl + c->pend[i].slot * BHRT_CTL_WORDS;
         if (!c->pend[i].redo) lost += w[6];
         if (!fold) continue;
@@ -564,7 +590,8 @@ static int harvest(devctx_t* c, int fold, hipStream_t st) {
             g_stats.frames_timed += 1;
         }
     }
-    c->npend = 0;
+    c->npend -= count;
+    if (c->npend > 0) memmove(c->pend, c->pend + count, (size_t)c->npend * sizeof c->pend[0]);
     if (lost) {
         set_err("%llu ray(s) needed the large-argument redo pass that the host had proved "
                 "unnecessary and left out: their outputs hold RAY_ERROR (BHRT_SKIP_REDO=0 "
@@ -582,7 +609,7 @@ int bhrt_get_stats(bhrt_stats* out, int reset) {
     for (int d = 0; d < BHRT_MAX_DEV; d++) {
         devctx_t* c = g_ctx[d];
         if (!c) continue;
-        if (harvest(c, out != NULL || !reset, NULL) != 0) rc = -1;
+        if (harvest(c, out != NULL || !reset, NULL, c->npend) != 0) rc = -1;
         if (c->span_on && c->span_hi > c->span_lo) span += c->span_hi - c->span_lo;
         if (reset) c->span_on = 0;
     }
@@ -856,7 +883,9 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     }
     /* the redo list follows the initial-state table (one extra field of the allocation) */
     kp->redo = (int*)(kp->init + (size_t)BHRT_INIT_FIELDS * (size_t)kp->n);
-    if (c->npend == BHRT_RING && harvest(c, 1, stream) != 0) return -1;
+    if (c->npend == BHRT_RING &&
+        harvest(c, 1, stream, env_int("BHRT_HARVEST_ALL", 0) ? BHRT_RING : BHRT_RING / 2) != 0)
+        return -1;
     if (ring_order(c, stream)) return -1;
     int slot = c->next_slot;
     c->next_slot = (c->next_slot + 1) % BHRT_RING;
@@ -879,8 +908,8 @@ static int launch(devctx_t* c, bhrt_kparams* kp, hipStream_t stream) {
     p->slot = slot;
     p->redo = !(kp->skip_redo && kp->no_evict);
     p->untested = bhrt_trace_untested(kp);
-    p->ev0 = c->evpool[2 * c->npend];
-    p->ev1 = c->evpool[2 * c->npend + 1];
+    p->ev0 = c->evpool[2 * slot]; /* (per slot: a slot has one pending launch at most) */
+    p->ev1 = c->evpool[2 * slot + 1];
     int e = bhrt_launch_trace(kp, (void*)stream, (void*)p->ev0, (void*)p->ev1);
     if (e != 0) {
         set_err("trace kernel launch failed: %s", hipGetErrorString((hipError_t)e));

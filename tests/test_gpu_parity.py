@@ -1263,3 +1263,49 @@ def test_control_ring_wraps(bhrt_lib):
     bhrt_lib.stats_discard()
     st = bhrt_lib.stats(reset=True)
     assert st["launches"] == 0 and st["rays"] == 0, st
+
+
+@pytest.mark.gpu
+def test_control_ring_wraps_across_streams(bhrt_lib):
+    """The ring-full launch harvests the older half of the control ring only and reuses it
+    (bhrt_api.c harvest): 700 frames rotating over three caller streams, no sync between them,
+    so the refilled half is zeroed on one stream while the newer half's frames still run on the
+    others, and every stream's first launch after the fill waits for it. Every frame must equal
+    the first bit for bit and the statistics must count every launch once."""
+    import torch
+    c = configs.CONFIGS["C4"]
+    bh, dk, cfg = c.scene()
+    cam = configs.camera("B")
+    W, H, frames = 16, 16, 700
+    n = W * H
+
+    def bufs():
+        return {f: torch.full((n,), 7, dtype=torch.int32 if f in ("result", "steps") else
+                              torch.float64, device="cuda") for f in abi.SOA_FIELDS}
+
+    first = bufs()
+    torch.cuda.synchronize()
+    bhrt_lib.stats(reset=True)
+    bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                 bhrt_lib.soa_from_tensors(first), None)
+    torch.cuda.synchronize()
+    one = bhrt_lib.stats(reset=True)
+    assert one["launches"] == 1 and one["rays"] == n, one
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    ring = [bufs() for _ in range(3)]
+    torch.cuda.synchronize()
+    soas = [bhrt_lib.soa_from_tensors(b) for b in ring]
+    for k in range(frames):
+        s = streams[k % 3]
+        bhrt_lib.render_frame_device(bh, dk, cfg, cam, W, H, None, c.method, c.flags,
+                                     soas[k % 3], s.cuda_stream)
+    torch.cuda.synchronize()
+    st = bhrt_lib.stats(reset=True)
+    assert st["launches"] == frames and st["rays"] == frames * n, st
+    assert st["iterations"] == frames * one["iterations"], (st, one)
+    for b in ring:
+        for f in abi.SOA_FIELDS:
+            assert torch.equal(b[f], first[f]) or (
+                b[f].dtype == torch.float64 and
+                torch.equal(torch.isnan(b[f]), torch.isnan(first[f])) and
+                torch.equal(b[f].nan_to_num(0.0), first[f].nan_to_num(0.0))), f
