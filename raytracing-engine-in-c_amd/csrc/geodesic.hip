@@ -943,17 +943,17 @@ __device__ __forceinline__ bool state_within(const Ray_& R, double bound) {
     return m <= bound;
 }
 
-// Where the step size is kept per ray with its r interval (ray_iterate): the RK4 Kerr path
-// (C4), whose ~80-VALU iteration spent 9 on the select chain: -3.6% kernel time same-box,
-// bit-identical (profiles/r03_ab/hcache_v33.txt). Elsewhere it measured neutral (C2, C5 --
-// where the changed code also moved some hit points by ~1e-15) or -1.4% (C3), so the chain
-// stays; k_path and the HUGE redo always select.
+// Where the step size is kept per ray with its r interval (ray_iterate): every RK4 path. C4's
+// ~80-VALU iteration spent 9 on the select chain: -3.6% kernel time same-box, bit-identical
+// (round 3). C2 measured neutral then; with round 6's wave-uniform trip it is +1.1% same-box,
+// bit-identical on C1 and C2 full frames (profiles/r06/ab_unroll.txt). RKF45 keeps the chain
+// (C3 -1.4%, C5 neutral in round 3); k_path and the HUGE redo always select.
 // The zero-acceleration paths (rotation_trig: C4, C5) keep it too, and form the rotation of
 // state[2]'s sin, cos for the new step size in the same rare branch: a regime change is then
 // one test per iteration instead of two.
 template <int METHOD, bool SPIN0, bool FAR, bool HUGE>
 constexpr bool hcache() {
-    return (METHOD == INTEGRATOR_RK4 && !SPIN0 && !HUGE) ||
+    return (METHOD == INTEGRATOR_RK4 && !HUGE) ||
            rotation_trig<METHOD, SPIN0, FAR, HUGE>();
 }
 
