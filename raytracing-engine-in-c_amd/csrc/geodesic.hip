@@ -1505,7 +1505,7 @@ __device__ unsigned long long g_stamps[kStampSlots * kStampWaves * kStampWords];
 #endif
 
 // Loop iterations per trip of the persistent loop (the HUGE redo pass keeps one): RKF45 with the
-// accept test 2, from same-box sweeps of 1..8 (round 2); RK4 a = 0 8 under a wave-uniform guard
+// accept test 2, from same-box sweeps of 1..8 (round 2); RK4 a = 0 4 under a wave-uniform guard
 // (uniform_trip; predicated, 10 measured C2 +0.3…0.5%, C1 +0.5…1% against round 2's 6 and 12 / 16
 // no better, profiles/r06/ab_unroll.txt). The zero-acceleration
 // paths' short iterations -- C4's RK4 step (~80 VALU) and C5's untested attempt (ACC, ~55) --
@@ -1516,13 +1516,14 @@ __device__ unsigned long long g_stamps[kStampSlots * kStampWaves * kStampWords];
 #define BHRT_UNROLL_ZA 16
 #endif
 #ifndef BHRT_UNROLL_A0
-#define BHRT_UNROLL_A0 8
+#define BHRT_UNROLL_A0 4
 #endif
 // The trip's later iterations under a wave-uniform guard (k_trace): RK4 a = 0 (C1, C2), whose
 // predicated form copies ~12 carried values (v_mov_b64) at the end of every iteration for the
-// lanes that stopped; 8 per trip (10 spill: 416 B scratch, C2 -65%). C1 +1.2%, C2 +0.4% against
-// the predicated 10 same-box; the zero-acceleration paths stay predicated (uniform: C4 -1%, C5
-// +-0; profiles/r06/ab_unroll.txt).
+// lanes that stopped. 8 per trip gave C1 +1.2%, C2 +0.4% against the predicated 10 same-box (10
+// spill: 416 B scratch, C2 -65%); with the per-ray step-size cache (hcache) shallower trips win:
+// 4 per trip, C2 +1.1%, C1 +4% against 8. The zero-acceleration paths stay predicated (uniform:
+// C4 -1%, C5 +-0; profiles/r06/ab_unroll.txt).
 template <int METHOD, bool SPIN0>
 constexpr bool uniform_trip() {
     return BHRT_UNIFORM_TRIP == 1 ||
