@@ -356,9 +356,11 @@ int bhrt_trace_rays(const Ray* rays, int n, const BlackHoleParams* blackhole,
 int bhrt_check_rkf45_accept(const double* err, const double* scale, const double* tol, int n,
                             int* out, void* hip_stream);
 
-/* Copy and optionally reset this thread's statistics (waits for the timed launches).
- * out == NULL with reset != 0 drops the pending launches' counters unread (no per-launch event
- * timing): the cheap reset before a timed region. */
+/* Copy and optionally reset this thread's statistics (waits for the timed launches, then reads
+ * their counters with a synchronous copy on the legacy default stream, i.e. also after the
+ * caller's default-stream work). out == NULL with reset != 0 drops the pending launches'
+ * counters unread (no per-launch event timing): the cheap reset before a timed region. Returns
+ * -1 if a launch whose redo pass was proved unnecessary handed a ray to it (bhrt_last_error). */
 int bhrt_get_stats(bhrt_stats* out, int reset);
 
 /* Number of GPUs libbhrt will use (HIP_VISIBLE_DEVICES / BHRT_MAX_DEVICES respected). */
