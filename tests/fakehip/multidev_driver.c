@@ -313,6 +313,33 @@ static void run(BlackHoleParams* bh, SimulationConfig* cfg, AccretionDiskParams*
     }
     bhrt_stats st;
     CHECK(bhrt_get_stats(&st, 1) == 0 && st.launches > 0 && st.rays > 0, "stats");
+    /* the control ring: 700 device frames over three streams with no wait between them. The
+     * launch that finds the ring full harvests its older half and reuses those slots (bhrt_api.c
+     * harvest); the launcher above adds each launch's rays to its slot's counter, so a slot
+     * reused without being zeroed, or a launch counted twice or never, shows in the total. */
+    {
+        const int W = 16, H = 8, frames = 700;
+        const long n = (long)W * H;
+        CHECK(hipSetDevice(0) == hipSuccess, "ring: device");
+        bhrt_frame_soa dev;
+        memset(&dev, 0, sizeof dev);
+        void** slot = (void**)&dev;
+        for (int f = 0; f < 15; f++)
+            if (ALL >> f & 1) CHECK(hipMalloc(&slot[f], fsize[f] * n) == hipSuccess, "ring: malloc");
+        hipStream_t s3[3];
+        for (int k = 0; k < 3; k++)
+            CHECK(hipStreamCreateWithFlags(&s3[k], 0) == hipSuccess, "ring: stream");
+        for (int k = 0; k < frames; k++)
+            CHECK(bhrt_render_frame_device(bh, dk, cfg, &cam, W, H, NULL, INTEGRATOR_RK4, 0, &dev,
+                                           s3[k % 3]) == 0,
+                  "ring: frame %d: %s", k, bhrt_last_error());
+        CHECK(bhrt_get_stats(&st, 1) == 0 && st.launches == (uint64_t)frames &&
+                  st.rays == (uint64_t)(frames * n),
+              "ring: %llu launches, %llu rays (want %d, %ld)", (unsigned long long)st.launches,
+              (unsigned long long)st.rays, frames, frames * n);
+        for (int f = 0; f < 15; f++)
+            if (slot[f]) hipFree(slot[f]);
+    }
 }
 
 static BlackHoleParams g_bh;
