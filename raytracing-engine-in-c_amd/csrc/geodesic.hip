@@ -1475,9 +1475,15 @@ constexpr int trace_waves_k() {
 // slot. A full 3-wave grid deals each wave ~10 blocks in its first (static) claim and loses 10%
 // against the 2-wave kernel; the 2-of-3 grid keeps ~16 blocks per wave and gains 11.6% (C3 13.1
 // -> 14.6 Grays/s same-box; 448 / 576 blocks +8% / -6%, profiles/r05/ab_occupancy_grid.txt).
-template <int METHOD, bool DISK, bool SPIN0, bool FAR, int INL>
+// The accept-all kernel (C5) launches 3 of its 4 resident waves per SIMD: +0.5...2.5% same-box
+// over three sessions at 16 attempts per trip (2, 2.5 and 3.5 waves per SIMD alike, C4 -2% at 3;
+// profiles/r06/ab_kernel_knobs.txt).
+#ifndef BHRT_ACC_LAUNCH_WAVES
+#define BHRT_ACC_LAUNCH_WAVES 3
+#endif
+template <int METHOD, bool DISK, bool SPIN0, bool FAR, int INL, bool ACC = false>
 constexpr int trace_launch_waves() {
-    return c3_camera<METHOD, DISK, SPIN0, FAR, false, INL>() ? 2 : 0;}
+    return c3_camera<METHOD, DISK, SPIN0, FAR, false, INL>() ? 2 : ACC ? BHRT_ACC_LAUNCH_WAVES : 0;}
 constexpr int BHRT_TRACE_WAVES_PER_BLOCK = 4;
 
 // Ray queues of k_trace: 64-id block b of the launch belongs to queue b mod 2^qbits; queue q's
@@ -2032,8 +2038,8 @@ void launch_trace_pair(const bhrt_kparams& kp, hipStream_t st) {
     // while launches of >= 16 tiles per wave lose 6-7% at half the grid (C3, C4 full, C5) and a
     // quarter grid loses against a half (profiles/r05/ab_grid_fraction.txt, ab_min_tiles.txt).
     // kp.grid_div > 0 overrides (BHRT_GRID_DIV).
-    if (trace_launch_waves<METHOD, DISK, SPIN0, FAR, INL>() > 0 && kp.grid_blocks <= 0) {
-        const int lw = device_cus(dev) * trace_launch_waves<METHOD, DISK, SPIN0, FAR, INL>() * 4 / (lanes / 64);
+    if (trace_launch_waves<METHOD, DISK, SPIN0, FAR, INL, ACC>() > 0 && kp.grid_blocks <= 0) {
+        const int lw = device_cus(dev) * trace_launch_waves<METHOD, DISK, SPIN0, FAR, INL, ACC>() * 4 / (lanes / 64);
         if (lw > 0 && lw < cap) cap = lw;
     }
     if (kp.grid_blocks > 0) {  // (A/B: an absolute grid, BHRT_GRID_BLOCKS)
